@@ -1,0 +1,240 @@
+"""bench.py -- radar frames/s of the MI355X FMCW path (BASELINE.json metric).
+
+One step = the whole hot path over one batch of device-resident synthetic
+frames (SURVEY.md 8d generator, seed 0xF3C0 ^ global frame index):
+range FFT + Doppler FFT for every range row (RD map written to HBM),
+detection, slow-time compaction, hop-1 STFT of the concatenated slow-time
+magnitude, global-max dB normalisation -- i.e. BASELINE.json config 4
+(config 3 + Hann(20) STFT, nfft 64) at 4096 frames of 256 x 1024 per GPU.
+For N > 1 GPUs each rank owns its own 4096-frame shard (weak scaling); the
+STFT halo, global max and range_speed gather run as RCCL collectives.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--fp16]
+
+Rank 0 prints one JSON line (contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "radar frames/sec (range-FFT+Doppler+STFT) + achieved HBM GB/s vs roofline"
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+STFT_WLEN, STFT_NOVERLAP, STFT_NFFT = 20, 19, 64
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=4096, help="frames per GPU per step")
+    ap.add_argument("--fp16", action="store_true", help="config-4 fp16 storage variant")
+    ap.add_argument("--chunk", type=int, default=0, help="frames per range/Doppler chunk (0 = library default)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-stage-timing", action="store_true")
+    ap.add_argument("--no-fanout", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from fmcw_radar_processing_amd import FMCW_C32H, FMCW_C64
+    from fmcw_radar_processing_amd import dist as fdist
+    from fmcw_radar_processing_amd import params as P
+    from fmcw_radar_processing_amd.engine import Engine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = P.config(4)                       # 1024 samples x 256 chirps, Nr 1024, Nd 256, throughput mode
+    F = args.frames
+    C, S, NR, ND = cfg.pn, cfg.nts, cfg.nr, cfg.nd
+    dt = FMCW_C32H if args.fp16 else FMCW_C64
+    tdt = torch.float16 if args.fp16 else torch.float32
+    eng = Engine(local)
+    eng.set_taps(cfg, P.synth_calibration(S))
+    if args.chunk:
+        eng.set_chunk_frames(args.chunk)
+    stream = torch.cuda.current_stream(dev)
+
+    # ---- device-resident input + outputs ------------------------------------------
+    d_iq = torch.empty((F, C, S, 2), dtype=tdt, device=dev)
+    eng.synth_device(d_iq, rank * F, F, dt, stream=stream)
+    M = cfg.max_targets
+    outs = dict(profile=torch.empty((F, NR), device=dev), tgt_count=torch.empty(F, dtype=torch.int32, device=dev),
+                tgt_range_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
+                tgt_range_mag=torch.empty((F, M), device=dev),
+                tgt_doppler_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
+                slow_mag=torch.empty((F, C), device=dev))
+    d_rd = torch.empty((F, NR, ND, 2), dtype=tdt, device=dev)
+    win = torch.tensor(cfg.stft_window(), dtype=torch.float32, device=dev)
+    fs = 1.0 / cfg.prt
+    h = STFT_WLEN - 1
+    max_seg = F * C + h
+    nb = STFT_NFFT // 2 + 1
+    flist = torch.empty(F, dtype=torch.int32, device=dev)
+    d_len = torch.zeros(1, dtype=torch.int64, device=dev)
+    d_P = torch.empty((max_seg, nb), dtype=torch.float32, device=dev)
+    pmax = torch.zeros(1, dtype=torch.float32, device=dev)
+    nseg = torch.zeros(1, dtype=torch.int64, device=dev)
+    halo = torch.zeros(h, dtype=torch.float32, device=dev)
+    halo_len = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        eng.process_device(d_iq, F, dt, outs, d_rd=d_rd, out_dtype=dt, stream=stream)
+        eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
+        hl, hbuf = None, None
+        if world > 1:
+            lens = fdist.all_lengths(d_len)
+            head = fdist.head_samples(outs["slow_mag"], flist, d_len, h)
+            hbuf, hl = fdist.right_halo(head, lens, rank)
+        pmax.zero_()
+        eng.stft_power_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
+                              max_seg, d_P, pmax, nseg, d_halo=hbuf, n_halo=h if world > 1 else 0,
+                              d_halo_len=hl, stream=stream)
+        if world > 1:
+            fdist.global_max_(pmax)
+        eng.stft_db_device(d_P, nseg, max_seg, STFT_NFFT, fs, pmax, 0, d_P, stream=stream)
+        if world > 1:
+            fdist.gather_range_speed(outs["tgt_count"], outs["tgt_range_idx"], outs["tgt_doppler_idx"],
+                                     outs["tgt_range_mag"])
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    level = 0 if args.no_stage_timing else 1
+    eng.timing(level)
+    eng.timing_reset()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    stages = eng.timing_read() if level else {}
+    eng.timing(0)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+
+    # sanity: the step did real work (detections on most frames)
+    det = int((outs["tgt_count"] > 0).sum().item())
+
+    # ---- roofline of the range+Doppler chunk (K1 range FFT + K2 Doppler FFT) --------
+    esz = 4 if args.fp16 else 8
+    alg_per_frame = C * S * esz + NR * ND * esz + NR * 4 + C * 4    # in + RD + profile + slow row
+    roof = None
+    rd_ms, rd_n = stages.get("range_doppler", (0.0, 0))
+    if rd_n:
+        per_launch_ms = rd_ms / rd_n
+        frames_per_launch = F * args.steps / rd_n
+        achieved = alg_per_frame * frames_per_launch / (per_launch_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                "kernel": "range+Doppler span: k_range || k_doppler chunk pipeline over 3 HIP streams "
+                          "(HIP events: before first k_range .. after last k_doppler)",
+                "avg_launch_us": round(per_launch_ms * 1e3, 2), "frames_per_launch": frames_per_launch,
+                "alg_bytes_per_frame": alg_per_frame}
+
+    # ---- input fan-out over xGMI from rank 0 (reported separately, not in value) -----
+    fanout = None
+    if world > 1 and not args.no_fanout:
+        nf = 256
+        src = torch.empty((world * nf, C, S, 2), dtype=tdt, device=dev) if rank == 0 else None
+        dst = torch.empty((nf, C, S, 2), dtype=tdt, device=dev)
+        parts = list(src.chunk(world)) if rank == 0 else None
+        dist.scatter(dst, parts, src=0)
+        torch.cuda.synchronize(dev)
+        barrier()
+        t1 = time.perf_counter()
+        dist.scatter(dst, parts, src=0)
+        torch.cuda.synchronize(dev)
+        barrier()
+        ft = time.perf_counter() - t1
+        fanout = {"frames_per_rank": nf, "ms": round(ft * 1e3, 3),
+                  "GBps_root_egress": round(world * nf * C * S * esz / ft / 1e9, 1)}
+        del src, dst
+
+    if rank == 0:
+        cpu = cpu_baseline(args.cpu_seconds) if args.cpu_seconds > 0 else None
+        total_frames = world * F * args.steps
+        value = total_frames / elapsed
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f16-storage/f32-compute" if args.fp16 else "f32",
+            "data": "synthetic (SURVEY.md 8d generator, generated in HBM per rank)",
+            "config": {"workload": "BASELINE config 4: per GPU 4096 frames x 256 chirps x 1024 samples; "
+                                   "range FFT 1024 + Doppler FFT 256 on every row + detection + "
+                                   "Hann(20) hop-1 STFT nfft 64 + dB", "frames_per_gpu": F,
+                       "chirps": C, "samples": S, "nr": NR, "nd": ND, "stft_nfft": STFT_NFFT,
+                       "parallelism": f"frame-shard dp{world}"},
+            "hbm_alg_GBps": round(alg_per_frame * value / world / 1e9, 1),
+            "roofline": roof,
+            "cpu_baseline": cpu,
+            "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items() if v[1]},
+            "frames_with_target": det,
+        }
+        if fanout:
+            line["input_fanout"] = fanout
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(budget_s: float):
+    """Oracle (fp64 numpy restatement of radar_processing.m:197-299) on a bounded
+    sample of the same config-4 workload, on this host, 1 thread."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    from fmcw_radar_processing_amd import params as P
+    from oracle import oracle as O
+    cfg = P.config(4)
+    p = O.derive_params(P.deployed_device(cfg.nts, cfg.pn), nr=cfg.nr, nd=cfg.nd, parity=False)
+    wr, wd = O.windows(cfg.nts, cfg.pn)
+    cal = O.synth_cal(cfg.nts)
+    win = O.stft_window("hann")
+    done, slow, busy = 0, [], 0.0
+    while busy < budget_s or done < 8:
+        iq = O.synth_frames(4, cfg.pn, cfg.nts, cfg.nr, cfg.nd, p["dist_per_bin"], frame0=done)  # not timed
+        t = time.perf_counter()
+        out = O.process_frames(iq, cal, p, wr, wd, rd_all_rows=True)
+        slow.append(O.slow_time_signal(out))
+        busy += time.perf_counter() - t
+        done += 4
+    t = time.perf_counter()
+    x = np.concatenate(slow)
+    if len(x) >= STFT_WLEN:
+        O.spectrogram_pipeline(x, cfg.prt, win, STFT_NOVERLAP, nfft=STFT_NFFT, nbins=0)
+    elapsed = busy + time.perf_counter() - t
+    return {"value": round(done / elapsed, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{done} frames of the config-4 workload through oracle/oracle.py "
+                      "(fp64 numpy restatement, 1 thread)"}
+
+
+if __name__ == "__main__":
+    main()

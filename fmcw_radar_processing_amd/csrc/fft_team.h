@@ -1,0 +1,245 @@
+// fft_team.h -- register/LDS FFT building block for gfx950 (wave64).
+//
+// An N-point forward FFT (N a power of two, 2..2048) is executed by a *team*
+// of T = N/P threads, each holding P = min(N,16) complex values in VGPRs.
+// The transform is a Stockham autosort sequence of radix-16 passes followed
+// by one radix-2/4/8 pass (N = 16^a * R0), e.g. 1024 = 16*16*4, 256 = 16*16.
+// Inside a pass every thread does its butterflies entirely in registers; the
+// data exchange between passes goes through the team's LDS region, padded by
+// one complex every 16 so the stride-16 write of pass 1 is bank-conflict free
+// (ds_write_b64: 16-lane groups, bank = dword mod 32).
+//
+// Data distribution (the property the kernels are built on):
+//   on entry  thread t holds x[t + T*m], m = 0..P-1  ("cyclic")
+//   on exit   thread t holds X[t + T*m], m = 0..P-1
+// so global loads and stores of consecutive t are coalesced both ways.
+//
+// This replaces MATLAB's fft(...) calls at radar_processing.m:205 (range,
+// along samples) and :219 (Doppler, along chirps).  Twiddles come from a
+// per-size table tw[i] = exp(-2*pi*i*i/N) rounded once from float64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+namespace fmcw {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(fmaf(a.x, b.x, -a.y * b.y), fmaf(a.x, b.y, a.y * b.x));
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 mul_negi(float2 a) { return make_float2(a.y, -a.x); }  // a * (-i)
+__device__ __forceinline__ float cabs2(float2 a) { return fmaf(a.x, a.x, a.y * a.y); }
+
+// ---- element I/O: complex float32 or complex float16 storage --------------
+__device__ __forceinline__ float2 ld_c(const float2* p, int64_t i) { return p[i]; }
+__device__ __forceinline__ float2 ld_c(const __half2* p, int64_t i) { return __half22float2(p[i]); }
+__device__ __forceinline__ void st_c(float2* p, int64_t i, float2 v) { p[i] = v; }
+__device__ __forceinline__ void st_c(__half2* p, int64_t i, float2 v) { p[i] = __float22half2_rn(v); }
+
+// ---- small forward DFTs in registers (natural order in and out) -----------
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+  const float2 t = a;
+  a = cadd(t, b);
+  b = csub(t, b);
+}
+
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = mul_negi(csub(a1, a3));
+  a0 = cadd(t0, t2);
+  a2 = csub(t0, t2);
+  a1 = cadd(t1, t3);
+  a3 = csub(t1, t3);
+}
+
+template <int R> __device__ __forceinline__ void dft(float2* v);
+
+template <> __device__ __forceinline__ void dft<1>(float2*) {}
+template <> __device__ __forceinline__ void dft<2>(float2* v) { dft2(v[0], v[1]); }
+template <> __device__ __forceinline__ void dft<4>(float2* v) { dft4(v[0], v[1], v[2], v[3]); }
+
+template <> __device__ __forceinline__ void dft<8>(float2* v) {
+  // radix-2 DIT over two 4-point DFTs of the even and odd samples
+  float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+  dft4(e0, e1, e2, e3);
+  dft4(o0, o1, o2, o3);
+  const float h = 0.70710678118654752440f;
+  o1 = make_float2(h * (o1.x + o1.y), h * (o1.y - o1.x));    // * W8^1 = h(1 - i)
+  o2 = mul_negi(o2);                                         // * W8^2 = -i
+  o3 = make_float2(h * (o3.y - o3.x), -h * (o3.x + o3.y));   // * W8^3 = h(-1 - i)
+  v[0] = cadd(e0, o0); v[4] = csub(e0, o0);
+  v[1] = cadd(e1, o1); v[5] = csub(e1, o1);
+  v[2] = cadd(e2, o2); v[6] = csub(e2, o2);
+  v[3] = cadd(e3, o3); v[7] = csub(e3, o3);
+}
+
+template <> __device__ __forceinline__ void dft<16>(float2* v) {
+  // X[k1 + 4 k2] = sum_n2 W4^(n2 k2) W16^(n2 k1) sum_n1 x[4 n1 + n2] W4^(n1 k1)
+  float2 y[16];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+    float2 a0 = v[n2], a1 = v[4 + n2], a2 = v[8 + n2], a3 = v[12 + n2];
+    dft4(a0, a1, a2, a3);
+    y[4 * n2 + 0] = a0; y[4 * n2 + 1] = a1; y[4 * n2 + 2] = a2; y[4 * n2 + 3] = a3;
+  }
+  // twiddles W16^m, m = n2*k1 in {1,2,3,2,4,6,3,6,9}
+  const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f, h = 0.70710678118654752440f;
+  y[5] = cmul(y[5], make_float2(c1, -s1));    // n2=1,k1=1: W^1
+  y[6] = cmul(y[6], make_float2(h, -h));      // n2=1,k1=2: W^2
+  y[7] = cmul(y[7], make_float2(s1, -c1));    // n2=1,k1=3: W^3
+  y[9] = cmul(y[9], make_float2(h, -h));      // n2=2,k1=1: W^2
+  y[10] = mul_negi(y[10]);                    // n2=2,k1=2: W^4 = -i
+  y[11] = cmul(y[11], make_float2(-h, -h));   // n2=2,k1=3: W^6
+  y[13] = cmul(y[13], make_float2(s1, -c1));  // n2=3,k1=1: W^3
+  y[14] = cmul(y[14], make_float2(-h, -h));   // n2=3,k1=2: W^6
+  y[15] = cmul(y[15], make_float2(-c1, s1));  // n2=3,k1=3: W^9
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    float2 a0 = y[k1], a1 = y[4 + k1], a2 = y[8 + k1], a3 = y[12 + k1];
+    dft4(a0, a1, a2, a3);
+    v[k1] = a0; v[k1 + 4] = a1; v[k1 + 8] = a2; v[k1 + 12] = a3;
+  }
+}
+
+// ---- plan --------------------------------------------------------------------
+template <int N> struct FftPlan {
+  static_assert(N >= 2 && N <= 4096 && (N & (N - 1)) == 0, "FFT size must be a power of two");
+  static constexpr int P = N < 16 ? N : 16;   // values per thread
+  static constexpr int T = N / P;             // threads per team
+  static constexpr int LDS = (N < 16) ? 0 : N + N / 16;  // complex elements of LDS per team
+};
+
+__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
+
+// Twiddle w^r (r = 1..R-1) for a pass, with w = tw[k * stride].  Only w^1, w^2,
+// w^4, w^8 come from the table; the others are formed with at most two
+// complex products (fewer loads in flight, fewer VGPRs, error <= ~3 ulp).
+template <int R>
+__device__ __forceinline__ void pass_twiddles(float2* w, const float2* __restrict__ tw, int base, int mask) {
+  w[1] = tw[base & mask];
+  if constexpr (R > 2) w[2] = tw[(2 * base) & mask];
+  if constexpr (R > 2) w[3] = cmul(w[1], w[2]);
+  if constexpr (R > 4) {
+    w[4] = tw[(4 * base) & mask];
+    w[5] = cmul(w[4], w[1]); w[6] = cmul(w[4], w[2]); w[7] = cmul(w[4], w[3]);
+  }
+  if constexpr (R > 8) {
+    w[8] = tw[(8 * base) & mask];
+#pragma unroll
+    for (int r = 9; r < 16; ++r) w[r] = cmul(w[8], w[r - 8]);
+  }
+}
+
+// One Stockham pass of radix R with stride Ns on registers in butterfly layout
+// v[q*R + r] = in[t + T*q + r*N/R].  Applies the inter-pass twiddles and the
+// radix-R DFTs in place.
+template <int N, int R, int Ns>
+__device__ __forceinline__ void stockham_pass_regs(float2* v, int t, const float2* __restrict__ tw) {
+  constexpr int P = FftPlan<N>::P, T = FftPlan<N>::T, Q = P / R;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    if constexpr (Ns > 1) {
+      const int j = t + T * q;
+      const int k = j & (Ns - 1);
+      float2 w[R];
+      pass_twiddles<R>(w, tw, k * (N / (Ns * R)), N - 1);
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], w[r]);
+    }
+    dft<R>(v + q * R);
+  }
+}
+
+// Write the pass output to LDS: out[(j/Ns)*Ns*R + j%Ns + r*Ns] = v[q*R + r].
+template <int N, int R, int Ns>
+__device__ __forceinline__ void stockham_store_lds(const float2* v, int t, float2* lds) {
+  constexpr int P = FftPlan<N>::P, T = FftPlan<N>::T, Q = P / R;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int j = t + T * q;
+    const int base = (j / Ns) * Ns * R + (j & (Ns - 1));
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[lds_pad(base + r * Ns)] = v[q * R + r];
+  }
+}
+
+// Read the next pass's input from LDS: v[q*R + r] = in[t + T*q + r*N/R].
+template <int N, int R>
+__device__ __forceinline__ void stockham_load_lds(float2* v, int t, const float2* lds) {
+  constexpr int P = FftPlan<N>::P, T = FftPlan<N>::T, Q = P / R;
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[q * R + r] = lds[lds_pad(t + T * q + r * (N / R))];
+}
+
+constexpr int fft_num_r16(int n) { return n >= 16 ? 1 + fft_num_r16(n / 16) : 0; }
+constexpr int fft_pow16(int k) { return k == 0 ? 1 : 16 * fft_pow16(k - 1); }
+
+// Recursive pass driver.  `PASS` indexes the pass, Ns = product of radices so far.
+template <int N, int PASS, int Ns, class Sync>
+__device__ __forceinline__ void team_fft_passes(float2* v, float2* lds, int t, const float2* __restrict__ tw,
+                                                Sync sync) {
+  constexpr int NR16 = fft_num_r16(N);
+  constexpr int R0 = N / fft_pow16(NR16);           // remainder radix (1, 2, 4, 8)
+  constexpr int NPASS = NR16 + (R0 > 1 ? 1 : 0);
+  constexpr int R = (PASS < NR16) ? 16 : R0;
+  constexpr int P = FftPlan<N>::P, Q = P / R;
+  stockham_pass_regs<N, R, Ns>(v, t, tw);
+  if constexpr (PASS + 1 < NPASS) {
+    constexpr int RN = (PASS + 1 < NR16) ? 16 : R0;
+    sync();                      // previous readers of `lds` are done (WAR)
+    stockham_store_lds<N, R, Ns>(v, t, lds);
+    sync();                      // stores visible (RAW)
+    stockham_load_lds<N, RN>(v, t, lds);
+    team_fft_passes<N, PASS + 1, Ns * R, Sync>(v, lds, t, tw, sync);
+  } else {
+    // last pass: the butterfly layout v[q*R + r] holds X[t + T*(q + r*Q)];
+    // permute to the cyclic layout v[m] = X[t + T*m] (compile-time moves).
+    if constexpr (Q > 1) {
+      float2 w[P];
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int r = 0; r < R; ++r) w[q + r * Q] = v[q * R + r];
+#pragma unroll
+      for (int m = 0; m < P; ++m) v[m] = w[m];
+    }
+  }
+}
+
+// Forward FFT of N points by a team; see the header comment for layouts.
+// `lds` is the team's private region of FftPlan<N>::LDS complex elements;
+// `sync` must order LDS accesses of all threads of the team.
+template <int N, class Sync>
+__device__ __forceinline__ void team_fft(float2* v, float2* lds, int t, const float2* __restrict__ tw, Sync sync) {
+  team_fft_passes<N, 0, 1, Sync>(v, lds, t, tw, sync);
+}
+
+struct BlockSync {
+  __device__ __forceinline__ void operator()() const { __syncthreads(); }
+};
+
+// A team that lives inside one wave only needs the wave's LDS accesses
+// ordered: LDS executes one wave's instructions in order, so a compiler
+// barrier with wavefront-scope fences is enough (no s_barrier).
+struct WaveSync {
+  __device__ __forceinline__ void operator()() const {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+};
+
+template <int T> struct TeamSync { using type = BlockSync; };
+template <> struct TeamSync<1> { using type = WaveSync; };
+template <> struct TeamSync<2> { using type = WaveSync; };
+template <> struct TeamSync<4> { using type = WaveSync; };
+template <> struct TeamSync<8> { using type = WaveSync; };
+template <> struct TeamSync<16> { using type = WaveSync; };
+template <> struct TeamSync<32> { using type = WaveSync; };
+template <> struct TeamSync<64> { using type = WaveSync; };
+
+}  // namespace fmcw

@@ -1,0 +1,750 @@
+// fmcw_api.cpp -- libfmcw C-ABI (include/fmcw.h) on top of the gfx950 kernels.
+//
+// Host responsibilities kept here, mirroring what radar_processing.m does
+// around the loop: argument validation (MATLAB would raise), twiddle tables,
+// scratch management for the per-chunk range cube, the chunked launch
+// sequence K1 -> K2 -> K3, the STFT size rules of :273/:276 and the
+// logspace/interp1 bin table of :293-299.
+#include "../../include/fmcw.h"
+#include "fmcw_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) return fail(FMCW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define CHK(expr)            \
+  do {                       \
+    int r_ = (expr);         \
+    if (r_ != FMCW_OK) return r_; \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= n && p) return FMCW_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (bytes == 0) bytes = 16;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(FMCW_E_OOM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    }
+    n = bytes;
+    return FMCW_OK;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+};
+
+size_t esize(int dtype) { return dtype == FMCW_C32H ? 4 : 8; }
+
+constexpr int kStages = 8;   // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call
+
+}  // namespace
+
+struct fmcw_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  // software pipeline over chunks: K1 (range) on the caller's stream, K2
+  // (Doppler) on sd, K3 (detect) on sx; chunk i's K2 overlaps chunk i+1's K1
+  static constexpr int kSlots = 3;
+  hipStream_t sd = nullptr, sx = nullptr;
+  hipEvent_t ev_k1[kSlots] = {}, ev_k2[kSlots] = {}, ev_k3[kSlots] = {};
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  bool taps = false;
+  fmcw_params p{};
+  DevBuf cal, calw, wd, tw_nr, tw_nd;
+  std::vector<float> h_wr, h_cal;   // host copies to rebuild calw when IF_scale changes
+  float calw_scale = 0.f;
+  float2 cal_sum{0.f, 0.f};
+  DevBuf scratch_cube, scratch_rd;
+  // host-pointer API staging
+  DevBuf h_iq, h_prof, h_count, h_ridx, h_rmag, h_didx, h_slow, h_cube, h_rd, h_probe;
+  DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
+  int64_t chunk_frames = 0;
+  int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
+  struct Pending {
+    hipEvent_t a, b;
+    int stage;
+  };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  double total_ms[kStages] = {};
+  int64_t launches[kStages] = {};
+
+  ~fmcw_ctx() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& pd : pending) { (void)hipEventDestroy(pd.a); (void)hipEventDestroy(pd.b); }
+    for (auto e : pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < kSlots; ++i)
+      for (hipEvent_t e : {ev_k1[i], ev_k2[i], ev_k3[i]})
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_fork, ev_join})
+      if (e) (void)hipEventDestroy(e);
+    for (hipStream_t x : {sd, sx})
+      if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  hipEvent_t get_event() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+};
+
+namespace {
+
+// Record an event pair around one launch when timing is enabled.
+struct StageTimer {
+  fmcw_ctx* c;
+  int stage;
+  hipStream_t s;
+  hipEvent_t a = nullptr;
+  StageTimer(fmcw_ctx* c_, int st, hipStream_t s_, int level = 1) : c(c_), stage(st), s(s_) {
+    if (c->timing >= level) {
+      a = c->get_event();
+      if (a) (void)hipEventRecord(a, s);
+    }
+  }
+  void done() {
+    if (a) {
+      hipEvent_t b = c->get_event();
+      if (b) {
+        (void)hipEventRecord(b, s);
+        c->pending.push_back({a, b, stage});
+      }
+      a = nullptr;
+    }
+  }
+};
+
+int set_device(fmcw_ctx* c) {
+  HIPCHK(hipSetDevice(c->device));
+  return FMCW_OK;
+}
+
+int check_params(const fmcw_params* p) {
+  if (!p) return fail(FMCW_E_ARG, "params is NULL");
+  if (p->nts < 1 || p->nts > 65536) return fail(FMCW_E_ARG, "nts out of range [1, 65536]");
+  if (p->pn < 1 || p->pn > 65536) return fail(FMCW_E_ARG, "pn out of range [1, 65536]");
+  if (!fmcw::range_size_supported(p->nr)) return fail(FMCW_E_ARG, "nr must be a power of two in [16, 2048]");
+  if (!fmcw::doppler_size_supported(p->nd)) return fail(FMCW_E_ARG, "nd must be a power of two in [2, 1024]");
+  if (p->max_targets < 1 || p->max_targets > 8) return fail(FMCW_E_ARG, "max_targets must be in [1, 8]");
+  if (!(p->dist_per_bin > 0.f)) return fail(FMCW_E_ARG, "dist_per_bin must be > 0");
+  return FMCW_OK;
+}
+
+// {cal.re, cal.im, IF_scale*w, w} per sample: one 16-byte load per sample in K1
+int build_calw(fmcw_ctx* c, float if_scale, hipStream_t s) {
+  const size_t n = c->h_wr.size();
+  std::vector<float> t(4 * n);
+  for (size_t i = 0; i < n; ++i) {
+    t[4 * i] = c->h_cal[2 * i];
+    t[4 * i + 1] = c->h_cal[2 * i + 1];
+    t[4 * i + 2] = (float)((double)if_scale * c->h_wr[i]);
+    t[4 * i + 3] = c->h_wr[i];
+  }
+  CHK(c->calw.ensure(t.size() * 4));
+  HIPCHK(hipMemcpyAsync(c->calw.p, t.data(), t.size() * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  c->calw_scale = if_scale;
+  return FMCW_OK;
+}
+
+int check_ctx(fmcw_ctx* c, const fmcw_params* p) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  CHK(check_params(p));
+  if (!c->taps) return fail(FMCW_E_STATE, "fmcw_set_taps has not been called");
+  if (p->nts != c->p.nts || p->pn != c->p.pn || p->nr != c->p.nr || p->nd != c->p.nd)
+    return fail(FMCW_E_STATE, "nts/pn/nr/nd differ from the ones given to fmcw_set_taps");
+  CHK(set_device(c));
+  if (p->if_scale != c->calw_scale) CHK(build_calw(c, p->if_scale, c->stream));
+  return FMCW_OK;
+}
+
+int upload_twiddles(DevBuf& buf, int n, hipStream_t s) {
+  std::vector<float> tw(2 * (size_t)n);
+  for (int i = 0; i < n; ++i) {
+    const double a = -2.0 * M_PI * (double)i / (double)n;
+    tw[2 * i] = (float)std::cos(a);
+    tw[2 * i + 1] = (float)std::sin(a);
+  }
+  CHK(buf.ensure(tw.size() * sizeof(float)));
+  HIPCHK(hipMemcpyAsync(buf.p, tw.data(), tw.size() * sizeof(float), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return FMCW_OK;
+}
+
+int64_t default_chunk(const fmcw_params* p) {
+  // The range cube of one chunk is the only intermediate: 64 MiB keeps it and
+  // the chunk's input/output streams inside the 256 MiB Infinity Cache.
+  const int64_t per_frame = (int64_t)p->pn * p->nr * 8;
+  int64_t c = (64ll << 20) / std::max<int64_t>(per_frame, 1);
+  return std::max<int64_t>(c, 1);
+}
+
+hipStream_t pick(fmcw_ctx* c, void* stream) { return stream ? static_cast<hipStream_t>(stream) : c->stream; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t fmcw_abi_version(void) { return FMCW_ABI_VERSION; }
+
+const char* fmcw_last_error(void) { return g_err.c_str(); }
+
+int fmcw_device_count(int32_t* n) {
+  if (!n) return fail(FMCW_E_ARG, "n is NULL");
+  int d = 0;
+  hipError_t e = hipGetDeviceCount(&d);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(FMCW_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *n = d;
+  return FMCW_OK;
+}
+
+int fmcw_ctx_create(int32_t device_id, fmcw_ctx** out) {
+  if (!out) return fail(FMCW_E_ARG, "out is NULL");
+  *out = nullptr;
+  int nd = 0;
+  HIPCHK(hipGetDeviceCount(&nd));
+  if (device_id < 0 || device_id >= nd)
+    return fail(FMCW_E_HIP, "device " + std::to_string(device_id) + " not present (" + std::to_string(nd) + " devices)");
+  HIPCHK(hipSetDevice(device_id));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device_id));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(FMCW_E_HIP, std::string("libfmcw is built for gfx950, device is ") + prop.gcnArchName);
+  auto* c = new fmcw_ctx();
+  c->device = device_id;
+  bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->sd, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->sx, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < fmcw_ctx::kSlots; ++i)
+    for (hipEvent_t* e : {&c->ev_k1[i], &c->ev_k2[i], &c->ev_k3[i]})
+      ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  for (hipEvent_t* e : {&c->ev_fork, &c->ev_join})
+    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    delete c;
+    return fail(FMCW_E_HIP, "stream/event creation failed");
+  }
+  *out = c;
+  return FMCW_OK;
+}
+
+int fmcw_ctx_destroy(fmcw_ctx* c) {
+  if (!c) return FMCW_OK;
+  delete c;
+  return FMCW_OK;
+}
+
+int fmcw_set_taps(fmcw_ctx* c, const fmcw_params* p, const float* range_win, const float* doppler_win,
+                  const float* calib) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  CHK(check_params(p));
+  if (!range_win || !doppler_win || !calib) return fail(FMCW_E_ARG, "taps pointer is NULL");
+  CHK(set_device(c));
+  hipStream_t s = c->stream;
+  CHK(c->wd.ensure((size_t)p->pn * 4));
+  CHK(c->cal.ensure((size_t)p->nts * 8));
+  HIPCHK(hipMemcpyAsync(c->wd.p, doppler_win, (size_t)p->pn * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->cal.p, calib, (size_t)p->nts * 8, hipMemcpyHostToDevice, s));
+  c->h_wr.assign(range_win, range_win + p->nts);
+  c->h_cal.assign(calib, calib + 2 * (size_t)p->nts);
+  double sr = 0, si = 0;
+  for (int n = 0; n < p->nts; ++n) { sr += calib[2 * n]; si += calib[2 * n + 1]; }
+  c->cal_sum = make_float2((float)sr, (float)si);
+  CHK(build_calw(c, p->if_scale, s));
+  CHK(upload_twiddles(c->tw_nr, p->nr, s));
+  CHK(upload_twiddles(c->tw_nd, p->nd, s));
+  c->p = *p;
+  c->taps = true;
+  return FMCW_OK;
+}
+
+int fmcw_set_chunk_frames(fmcw_ctx* c, int64_t frames) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (frames < 0) return fail(FMCW_E_ARG, "frames < 0");
+  c->chunk_frames = frames;
+  return FMCW_OK;
+}
+
+int fmcw_synchronize(fmcw_ctx* c) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  CHK(set_device(c));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return FMCW_OK;
+}
+
+int fmcw_timing_enable(fmcw_ctx* c, int32_t enable) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (enable < 0 || enable > 2) return fail(FMCW_E_ARG, "timing level must be 0, 1 or 2");
+  c->timing = enable;
+  return FMCW_OK;
+}
+
+static int timing_collect(fmcw_ctx* c) {
+  for (auto& pd : c->pending) {
+    HIPCHK(hipEventSynchronize(pd.b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, pd.a, pd.b));
+    c->total_ms[pd.stage] += ms;
+    c->launches[pd.stage] += 1;
+    c->pool.push_back(pd.a);
+    c->pool.push_back(pd.b);
+  }
+  c->pending.clear();
+  return FMCW_OK;
+}
+
+int fmcw_timing_read(fmcw_ctx* c, int32_t stage, double* total_ms, int64_t* launches) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (stage < 0 || stage >= kStages) return fail(FMCW_E_ARG, "stage out of range");
+  CHK(set_device(c));
+  CHK(timing_collect(c));
+  if (total_ms) *total_ms = c->total_ms[stage];
+  if (launches) *launches = c->launches[stage];
+  return FMCW_OK;
+}
+
+int fmcw_timing_reset(fmcw_ctx* c) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  CHK(set_device(c));
+  CHK(timing_collect(c));
+  for (int i = 0; i < kStages; ++i) { c->total_ms[i] = 0; c->launches[i] = 0; }
+  return FMCW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// per-frame stages
+// ---------------------------------------------------------------------------
+int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
+                        float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
+                        float* d_slow, void* d_cube, void* d_rd, int32_t out_dtype, int64_t probe_column,
+                        float* d_probe, void* stream) {
+  CHK(check_ctx(c, p));
+  if (F < 0) return fail(FMCW_E_ARG, "F < 0");
+  if (F == 0) return FMCW_OK;
+  if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
+  if (out_dtype != FMCW_C64 && out_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad out_dtype");
+  if (!d_iq || !d_prof || !d_count || !d_ridx || !d_rmag || !d_didx || !d_slow)
+    return fail(FMCW_E_ARG, "required device pointer is NULL");
+  const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
+  if (probe_column < 0 || probe_column > F * (int64_t)C) return fail(FMCW_E_ARG, "probe_column out of range");
+  hipStream_t s = pick(c, stream);
+  const int64_t chunk = c->chunk_frames > 0 ? c->chunk_frames : default_chunk(p);
+  const int cube_dt = d_cube ? out_dtype : FMCW_C64;
+  const int rd_dt = d_rd ? out_dtype : FMCW_C64;
+  // fp16 storage keeps MATLAB's values divided by the FFT sizes applied so far
+  // (exact powers of two): |X|/Nr and |D|/(Nr*Nd) stay inside the fp16 range
+  const float cube_scale = cube_dt == FMCW_C32H ? 1.0f / NR : 1.0f;
+  const float rd_scale = rd_dt == FMCW_C32H ? 1.0f / ((float)NR * ND) : 1.0f;
+  const int64_t cf = std::min(chunk, F);
+  const size_t cube_slot = (size_t)cf * C * NR * 8, rd_slot = (size_t)cf * NR * ND * 8;
+  constexpr int NS = fmcw_ctx::kSlots;
+  // NS scratch slots: while K3(i-1) and K2(i) read slots (i-1)%NS and i%NS,
+  // K1(i+1) fills slot (i+1)%NS
+  if (!d_cube) CHK(c->scratch_cube.ensure(NS * cube_slot));
+  if (!d_rd) CHK(c->scratch_rd.ensure(NS * rd_slot));
+  const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
+  const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
+  hipStream_t sd = c->sd, sx = c->sx;
+  StageTimer span(c, 7, s, 1);     // range+Doppler span: before K1(0) on s ... after the last K2 on sd
+  HIPCHK(hipEventRecord(c->ev_fork, s));
+  HIPCHK(hipStreamWaitEvent(sd, c->ev_fork, 0));
+  HIPCHK(hipStreamWaitEvent(sx, c->ev_fork, 0));
+
+  int64_t i = 0;
+  for (int64_t f0 = 0; f0 < F; f0 += chunk, ++i) {
+    const int b = (int)(i % NS);
+    const int64_t nf = std::min(chunk, F - f0);
+    if (i >= NS) HIPCHK(hipStreamWaitEvent(s, c->ev_k3[b], 0));   // WAR: K2/K3(i-NS) done with slot b
+    char* cube = d_cube ? static_cast<char*>(d_cube) + (size_t)f0 * C * NR * esize(cube_dt)
+                        : c->scratch_cube.as<char>() + b * cube_slot;
+    char* rd = d_rd ? static_cast<char*>(d_rd) + (size_t)f0 * NR * ND * esize(rd_dt)
+                    : c->scratch_rd.as<char>() + b * rd_slot;
+
+    fmcw::RangeArgs ra{};
+    ra.iq = static_cast<const char*>(d_iq) + (size_t)f0 * C * S * esize(in_dtype);
+    ra.in_dtype = in_dtype;
+    ra.nchirps = nf * C;
+    ra.C = C; ra.S = S; ra.NR = NR;
+    ra.calw = c->calw.as<float4>();
+    ra.cal_sum = c->cal_sum;
+    ra.if_scale = p->if_scale;
+    ra.tw = c->tw_nr.as<float2>();
+    ra.cube = cube;
+    ra.cube_dtype = cube_dt;
+    ra.cube_scale = cube_scale;
+    ra.profile = nullptr;
+    ra.cpt = 1;
+    {
+      StageTimer tm(c, 0, s, 2);
+      HIPCHK(fmcw::launch_range(ra, s));
+      tm.done();
+    }
+    HIPCHK(hipEventRecord(c->ev_k1[b], s));
+    HIPCHK(hipStreamWaitEvent(sd, c->ev_k1[b], 0));
+
+    fmcw::DopplerArgs da{};
+    da.cube = cube; da.cube_dtype = cube_dt;
+    da.cube_unscale = 1.0f / cube_scale; da.rd_scale = rd_scale;
+    da.nframes = (int)nf; da.C = C; da.NR = NR; da.ND = ND;
+    da.wd = c->wd.as<float>();
+    da.tw = c->tw_nd.as<float2>();
+    da.rd = rd; da.rd_dtype = rd_dt;
+    da.profile = d_prof + f0 * NR;
+    {
+      StageTimer tm(c, 1, sd, 2);
+      HIPCHK(fmcw::launch_doppler(da, sd));
+      tm.done();
+    }
+    HIPCHK(hipEventRecord(c->ev_k2[b], sd));
+    HIPCHK(hipStreamWaitEvent(sx, c->ev_k2[b], 0));
+
+    fmcw::DetectArgs ka{};
+    ka.profile = d_prof + f0 * NR;
+    ka.rd = rd; ka.rd_dtype = rd_dt;
+    ka.cube = cube; ka.cube_dtype = cube_dt;
+    ka.cube_unscale = 1.0f / cube_scale; ka.rd_unscale = 1.0f / rd_scale;
+    ka.nframes = (int)nf; ka.NR = NR; ka.ND = ND; ka.C = C; ka.M = M;
+    ka.range_thr = p->range_thr; ka.doppler_thr = p->doppler_thr;
+    ka.min_d = p->min_d; ka.max_d = p->max_d; ka.dist_per_bin = p->dist_per_bin;
+    ka.fallback = p->doppler_fallback_idx;
+    ka.count = d_count + f0;
+    ka.ridx = d_ridx + f0 * M;
+    ka.rmag = d_rmag + f0 * M;
+    ka.didx = d_didx + f0 * M;
+    ka.slow_mag = d_slow + f0 * C;
+    ka.probe_frame = (pframe >= f0 && pframe < f0 + nf) ? pframe - f0 : -1;
+    ka.probe_chirp = pchirp;
+    ka.probe_mag = d_probe;
+    {
+      StageTimer tm(c, 2, sx, 2);
+      HIPCHK(fmcw::launch_detect(ka, sx));
+      tm.done();
+    }
+    HIPCHK(hipEventRecord(c->ev_k3[b], sx));
+  }
+  span.s = sd;
+  span.done();
+  // join: the caller's stream waits for the last detect (which follows every K2)
+  HIPCHK(hipEventRecord(c->ev_join, sx));
+  HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+  return FMCW_OK;
+}
+
+int fmcw_range_fft_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
+                          void* d_cube, int32_t out_dtype, float* d_prof, void* stream) {
+  CHK(check_ctx(c, p));
+  if (F < 0) return fail(FMCW_E_ARG, "F < 0");
+  if (F == 0) return FMCW_OK;
+  if (!d_iq || !d_cube || !d_prof) return fail(FMCW_E_ARG, "required device pointer is NULL");
+  if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
+  if (out_dtype != FMCW_C64 && out_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad out_dtype");
+  hipStream_t s = pick(c, stream);
+  HIPCHK(hipMemsetAsync(d_prof, 0, (size_t)F * p->nr * 4, s));   // 0.0f: identity of max over |.|
+  fmcw::RangeArgs ra{};
+  ra.iq = d_iq; ra.in_dtype = in_dtype;
+  ra.nchirps = F * p->pn;
+  ra.C = p->pn; ra.S = p->nts; ra.NR = p->nr;
+  ra.calw = c->calw.as<float4>(); ra.cal_sum = c->cal_sum; ra.if_scale = p->if_scale;
+  ra.tw = c->tw_nr.as<float2>();
+  ra.cube = d_cube; ra.cube_dtype = out_dtype;
+  ra.cube_scale = out_dtype == FMCW_C32H ? 1.0f / p->nr : 1.0f;
+  ra.profile = d_prof;
+  int cpt = 16;
+  while (cpt > 1 && (p->pn % cpt) != 0) cpt >>= 1;
+  ra.cpt = cpt;
+  StageTimer tm(c, 6, s);
+  HIPCHK(fmcw::launch_range(ra, s));
+  tm.done();
+  return FMCW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// slow time + STFT
+// ---------------------------------------------------------------------------
+int fmcw_compact_device(fmcw_ctx* c, const int32_t* d_count, int64_t F, int32_t pn, int32_t* d_list,
+                        int64_t* d_len, void* stream) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (F < 0 || pn < 1) return fail(FMCW_E_ARG, "bad F / pn");
+  if (!d_count || !d_list || !d_len) return fail(FMCW_E_ARG, "NULL device pointer");
+  CHK(set_device(c));
+  hipStream_t s = pick(c, stream);
+  StageTimer tm(c, 3, s);
+  HIPCHK(fmcw::launch_compact(d_count, F, pn, d_list, d_len, s));
+  tm.done();
+  return FMCW_OK;
+}
+
+static int check_stft_shape(int32_t wlen, int32_t noverlap, int32_t nfft) {
+  if (wlen < 1 || wlen > 256) return fail(FMCW_E_ARG, "wlen must be in [1, 256]");
+  if (noverlap < 0 || noverlap >= wlen) return fail(FMCW_E_ARG, "noverlap must be in [0, wlen)");
+  if (nfft < wlen || (nfft % 2) != 0) return fail(FMCW_E_ARG, "nfft must be even and >= wlen");
+  return FMCW_OK;
+}
+
+int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_list, const int64_t* d_len,
+                           int32_t pn, const float* d_halo, int32_t n_halo, const int64_t* d_halo_len,
+                           const float* d_win, int32_t wlen,
+                           int32_t noverlap, int32_t nfft, double fs, int64_t max_seg, float* d_P, float* d_pmax,
+                           int64_t* d_nseg, void* stream) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  CHK(check_stft_shape(wlen, noverlap, nfft));
+  if (pn < 1 || n_halo < 0 || max_seg < 0 || !(fs > 0)) return fail(FMCW_E_ARG, "bad pn / n_halo / max_seg / fs");
+  if (!d_slow || !d_list || !d_len || !d_win || !d_P || !d_pmax || !d_nseg || (n_halo > 0 && !d_halo))
+    return fail(FMCW_E_ARG, "NULL device pointer");
+  CHK(set_device(c));
+  hipStream_t s = pick(c, stream);
+  fmcw::StftArgs a{};
+  a.slow_mag = d_slow; a.frame_list = d_list; a.len = d_len; a.pn = pn;
+  a.halo = d_halo; a.n_halo = n_halo; a.halo_len = d_halo_len;
+  a.win = d_win; a.wlen = wlen; a.hop = wlen - noverlap; a.nfft = nfft;
+  a.inv_fs = (float)(1.0 / fs);
+  a.max_seg = max_seg; a.P = d_P; a.pmax = d_pmax; a.nseg_out = d_nseg;
+  StageTimer tm(c, 4, s);
+  HIPCHK(fmcw::launch_stft_power(a, s));
+  tm.done();
+  return FMCW_OK;
+}
+
+// logspace(log10(fs/nfft), log10(fs/2), n) located on F = (0:nfft/2)*fs/nfft
+static void log_table(int nfft, double fs, int n, std::vector<int32_t>& idx, std::vector<float>& wt,
+                      std::vector<double>* fq_out) {
+  const int nb = nfft / 2 + 1;
+  const double df = fs / nfft;
+  const double a = std::log10(df), b = std::log10((nb - 1) * df);
+  idx.resize(n);
+  wt.resize(n);
+  if (fq_out) fq_out->resize(n);
+  for (int j = 0; j < n; ++j) {
+    const double e = (n == 1) ? b : (j == n - 1 ? b : a + j * (b - a) / (n - 1));
+    const double fq = std::pow(10.0, e);
+    int i0 = (int)std::floor(fq / df);
+    if (i0 < 0) i0 = 0;
+    if (i0 > nb - 2) i0 = nb - 2;
+    idx[j] = i0;
+    wt[j] = (float)((fq - i0 * df) / df);
+    if (fq_out) (*fq_out)[j] = fq;
+  }
+}
+
+int fmcw_stft_db_device(fmcw_ctx* c, const float* d_P, const int64_t* d_nseg, int64_t max_seg, int32_t nfft,
+                        double fs, const float* d_pmax, int32_t n_log_bins, float* d_out, void* stream) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (nfft < 2 || (nfft % 2) != 0 || n_log_bins < 0 || max_seg < 0 || !(fs > 0))
+    return fail(FMCW_E_ARG, "bad nfft / n_log_bins / max_seg / fs");
+  if (!d_P || !d_nseg || !d_pmax || !d_out) return fail(FMCW_E_ARG, "NULL device pointer");
+  if (n_log_bins > 0 && d_out == d_P) return fail(FMCW_E_ARG, "d_out may alias d_P only without resampling");
+  CHK(set_device(c));
+  hipStream_t s = pick(c, stream);
+  if (n_log_bins > 0) {
+    std::vector<int32_t> idx;
+    std::vector<float> wt;
+    log_table(nfft, fs, n_log_bins, idx, wt, nullptr);
+    CHK(c->s_lidx.ensure(idx.size() * 4));
+    CHK(c->s_lw.ensure(wt.size() * 4));
+    HIPCHK(hipMemcpyAsync(c->s_lidx.p, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->s_lw.p, wt.data(), wt.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));   // host vectors go out of scope
+  }
+  fmcw::StftDbArgs a{};
+  a.P = d_P; a.nseg = d_nseg; a.max_seg = max_seg; a.nbins_in = nfft / 2 + 1;
+  a.pmax = d_pmax; a.nlog = n_log_bins;
+  a.lidx = n_log_bins > 0 ? c->s_lidx.as<int32_t>() : nullptr;
+  a.lw = n_log_bins > 0 ? c->s_lw.as<float>() : nullptr;
+  a.out = d_out;
+  StageTimer tm(c, 5, s);
+  HIPCHK(fmcw::launch_stft_db(a, s));
+  tm.done();
+  return FMCW_OK;
+}
+
+int fmcw_stft_sizes(int64_t L, int32_t wlen, int32_t noverlap, int32_t nfft, int32_t n_log_bins, int64_t* nseg,
+                    int32_t* nfft_used, int32_t* nbins_out) {
+  if (L < 0 || n_log_bins < 0) return fail(FMCW_E_ARG, "L < 0 or n_log_bins < 0");
+  int32_t nf = nfft;
+  if (nf == 0) {                       // :273 nfft_stft = 2^nextpow2(length(iq_data(:)))
+    int64_t v = 1;
+    while (v < L) v <<= 1;
+    if (v > (1 << 26)) return fail(FMCW_E_ARG, "2^nextpow2(L) too large");
+    nf = (int32_t)v;
+  }
+  if (wlen < 1 || noverlap < 0 || noverlap >= wlen) return fail(FMCW_E_ARG, "need 0 <= noverlap < wlen");
+  const int hop = wlen - noverlap;
+  const int64_t ns = (L - noverlap) >= 0 ? (L - noverlap) / hop : 0;   // fix((nx-noverlap)/(nwind-noverlap))
+  if (nseg) *nseg = ns;
+  if (nfft_used) *nfft_used = nf;
+  if (nbins_out) *nbins_out = n_log_bins > 0 ? n_log_bins : nf / 2 + 1;
+  if (ns < 1) return fail(FMCW_E_DATA, "spectrogram: signal length " + std::to_string(L) + " is shorter than the window");
+  CHK(check_stft_shape(wlen, noverlap, nf));
+  return FMCW_OK;
+}
+
+int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap, int32_t nfft,
+              double fs, int32_t n_log_bins, float* T, float* freq, float* intensity) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if ((!x && L > 0) || !win || !T || !freq || !intensity) return fail(FMCW_E_ARG, "NULL pointer");
+  if (!(fs > 0)) return fail(FMCW_E_ARG, "fs must be > 0");
+  if (L > 0x7fffffffLL) return fail(FMCW_E_ARG, "L too large for the host API");
+  int64_t nseg = 0;
+  int32_t nf = 0, nbo = 0;
+  CHK(fmcw_stft_sizes(L, wlen, noverlap, nfft, n_log_bins, &nseg, &nf, &nbo));
+  CHK(set_device(c));
+  hipStream_t s = c->stream;
+  const int nb = nf / 2 + 1;
+  CHK(c->s_x.ensure((size_t)L * 4));
+  CHK(c->s_list.ensure(4));
+  CHK(c->s_len.ensure(8));
+  CHK(c->s_P.ensure((size_t)nseg * nb * 4));
+  CHK(c->s_pmax.ensure(4));
+  CHK(c->s_nseg.ensure(8));
+  CHK(c->s_win.ensure((size_t)wlen * 4));
+  CHK(c->s_out.ensure((size_t)nseg * nbo * 4));
+  const int32_t zero = 0;
+  const int64_t len = L;
+  HIPCHK(hipMemcpyAsync(c->s_x.p, x, (size_t)L * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->s_list.p, &zero, 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->s_len.p, &len, 8, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->s_win.p, win, (size_t)wlen * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(c->s_pmax.p, 0, 4, s));
+  // the whole signal is one "frame" of L samples in the compaction indirection
+  CHK(fmcw_stft_power_device(c, c->s_x.as<float>(), c->s_list.as<int32_t>(), c->s_len.as<int64_t>(), (int32_t)L,
+                             nullptr, 0, nullptr, c->s_win.as<float>(), wlen, noverlap, nf, fs, nseg, c->s_P.as<float>(),
+                             c->s_pmax.as<float>(), c->s_nseg.as<int64_t>(), s));
+  CHK(fmcw_stft_db_device(c, c->s_P.as<float>(), c->s_nseg.as<int64_t>(), nseg, nf, fs, c->s_pmax.as<float>(),
+                          n_log_bins, n_log_bins > 0 ? c->s_out.as<float>() : c->s_P.as<float>(), s));
+  const float* res = n_log_bins > 0 ? c->s_out.as<float>() : c->s_P.as<float>();
+  HIPCHK(hipMemcpyAsync(intensity, res, (size_t)nseg * nbo * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const int hop = wlen - noverlap;
+  for (int64_t i = 0; i < nseg; ++i) T[i] = (float)(((double)i * hop + wlen / 2.0) / fs);   // spectrogram T
+  if (n_log_bins > 0) {
+    std::vector<int32_t> idx;
+    std::vector<float> wt;
+    std::vector<double> fq;
+    log_table(nf, fs, n_log_bins, idx, wt, &fq);
+    for (int j = 0; j < n_log_bins; ++j) freq[j] = (float)fq[j];
+  } else {
+    for (int j = 0; j < nb; ++j) freq[j] = (float)(j * fs / nf);
+  }
+  return FMCW_OK;
+}
+
+// ---------------------------------------------------------------------------
+// host-pointer per-frame API
+// ---------------------------------------------------------------------------
+int fmcw_process(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F, float* prof,
+                 int32_t* count, int32_t* ridx, float* rmag, int32_t* didx, float* slow, float* cube, float* rd,
+                 int64_t probe_column, float* probe) {
+  CHK(check_ctx(c, p));
+  if (F < 0) return fail(FMCW_E_ARG, "F < 0");
+  if (F == 0) return FMCW_OK;
+  if (!iq || !prof || !count || !ridx || !rmag || !didx || !slow) return fail(FMCW_E_ARG, "required pointer is NULL");
+  if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
+  const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
+  hipStream_t s = c->stream;
+  CHK(c->h_iq.ensure((size_t)F * C * S * esize(in_dtype)));
+  CHK(c->h_prof.ensure((size_t)F * NR * 4));
+  CHK(c->h_count.ensure((size_t)F * 4));
+  CHK(c->h_ridx.ensure((size_t)F * M * 4));
+  CHK(c->h_rmag.ensure((size_t)F * M * 4));
+  CHK(c->h_didx.ensure((size_t)F * M * 4));
+  CHK(c->h_slow.ensure((size_t)F * C * 4));
+  if (cube) CHK(c->h_cube.ensure((size_t)F * C * NR * 8));
+  if (rd) CHK(c->h_rd.ensure((size_t)F * NR * ND * 8));
+  if (probe) CHK(c->h_probe.ensure((size_t)NR * 4));
+  HIPCHK(hipMemcpyAsync(c->h_iq.p, iq, (size_t)F * C * S * esize(in_dtype), hipMemcpyHostToDevice, s));
+  CHK(fmcw_process_device(c, p, c->h_iq.p, in_dtype, F, c->h_prof.as<float>(), c->h_count.as<int32_t>(),
+                          c->h_ridx.as<int32_t>(), c->h_rmag.as<float>(), c->h_didx.as<int32_t>(), c->h_slow.as<float>(),
+                          cube ? c->h_cube.p : nullptr, rd ? c->h_rd.p : nullptr, FMCW_C64, probe ? probe_column : 0,
+                          probe ? c->h_probe.as<float>() : nullptr, s));
+  HIPCHK(hipMemcpyAsync(prof, c->h_prof.p, (size_t)F * NR * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(count, c->h_count.p, (size_t)F * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(ridx, c->h_ridx.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(rmag, c->h_rmag.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(didx, c->h_didx.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(slow, c->h_slow.p, (size_t)F * C * 4, hipMemcpyDeviceToHost, s));
+  if (cube) HIPCHK(hipMemcpyAsync(cube, c->h_cube.p, (size_t)F * C * NR * 8, hipMemcpyDeviceToHost, s));
+  if (rd) HIPCHK(hipMemcpyAsync(rd, c->h_rd.p, (size_t)F * NR * ND * 8, hipMemcpyDeviceToHost, s));
+  if (probe) HIPCHK(hipMemcpyAsync(probe, c->h_probe.p, (size_t)NR * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return FMCW_OK;
+}
+
+int fmcw_range_fft(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F, float* cube,
+                   float* prof) {
+  CHK(check_ctx(c, p));
+  if (F < 0) return fail(FMCW_E_ARG, "F < 0");
+  if (F == 0) return FMCW_OK;
+  if (!iq || !cube || !prof) return fail(FMCW_E_ARG, "required pointer is NULL");
+  if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
+  const int S = p->nts, C = p->pn, NR = p->nr;
+  hipStream_t s = c->stream;
+  CHK(c->h_iq.ensure((size_t)F * C * S * esize(in_dtype)));
+  CHK(c->h_cube.ensure((size_t)F * C * NR * 8));
+  CHK(c->h_prof.ensure((size_t)F * NR * 4));
+  HIPCHK(hipMemcpyAsync(c->h_iq.p, iq, (size_t)F * C * S * esize(in_dtype), hipMemcpyHostToDevice, s));
+  CHK(fmcw_range_fft_device(c, p, c->h_iq.p, in_dtype, F, c->h_cube.p, FMCW_C64, c->h_prof.as<float>(), s));
+  HIPCHK(hipMemcpyAsync(cube, c->h_cube.p, (size_t)F * C * NR * 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(prof, c->h_prof.p, (size_t)F * NR * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return FMCW_OK;
+}
+
+int fmcw_synth_device(fmcw_ctx* c, const fmcw_params* p, int64_t frame0, int64_t F, void* d_iq, int32_t dtype,
+                      void* stream) {
+  CHK(check_ctx(c, p));
+  if (F < 0 || frame0 < 0) return fail(FMCW_E_ARG, "F / frame0 < 0");
+  if (!d_iq) return fail(FMCW_E_ARG, "d_iq is NULL");
+  if (dtype != FMCW_C64 && dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad dtype");
+  fmcw::SynthArgs a{};
+  a.iq = d_iq; a.dtype = dtype; a.frame0 = frame0; a.nframes = F;
+  a.C = p->pn; a.S = p->nts; a.NR = p->nr; a.ND = p->nd;
+  a.dist_per_bin = p->dist_per_bin;
+  a.cal = c->cal.as<float2>();
+  HIPCHK(fmcw::launch_synth(a, pick(c, stream)));
+  return FMCW_OK;
+}
+
+}  // extern "C"

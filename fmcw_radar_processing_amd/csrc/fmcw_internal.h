@@ -1,0 +1,108 @@
+// fmcw_internal.h -- launch wrappers shared by kernels_*.hip and fmcw_api.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fmcw {
+
+struct RangeArgs {
+  const void* iq;          // [nchirps][S] complex, dtype in_dtype
+  int in_dtype;            // FMCW_C64 / FMCW_C32H
+  int64_t nchirps;         // chirps in this launch (= frames * C)
+  int C, S, NR;
+  const float4* calw;      // [S] {cal.re, cal.im, if_scale*w, w}  (w = 2*blackman)
+  float2 cal_sum;          // sum_n cal[n] over all S samples
+  float if_scale;
+  const float2* tw;        // [NR]
+  void* cube;              // [nchirps][NR], dtype cube_dtype
+  int cube_dtype;
+  float cube_scale;        // stored value = X * cube_scale (1, or 1/NR for fp16)
+  float* profile;          // [frames][NR] (max over chirps, atomically raised) or nullptr
+  int cpt;                 // chirps per team (divides C when profile != nullptr)
+};
+
+struct DopplerArgs {
+  const void* cube;        // [frames][C][NR]
+  int cube_dtype;
+  float cube_unscale;      // 1/cube_scale
+  float rd_scale;          // stored value = D * rd_scale (1, or 1/(NR*ND) for fp16)
+  int nframes, C, NR, ND;
+  const float* wd;         // [C]
+  const float2* tw;        // [ND]
+  void* rd;                // [frames][NR][ND]
+  int rd_dtype;
+  float* profile;          // [frames][NR]
+};
+
+struct DetectArgs {
+  const float* profile;    // [frames][NR]
+  const void* rd;          // [frames][NR][ND]
+  int rd_dtype;
+  const void* cube;        // [frames][C][NR]
+  int cube_dtype;
+  float cube_unscale, rd_unscale;
+  int nframes, NR, ND, C, M;
+  float range_thr, doppler_thr, min_d, max_d, dist_per_bin;
+  int fallback;
+  int32_t* count;          // [frames]
+  int32_t* ridx;           // [frames][M]
+  float* rmag;             // [frames][M]
+  int32_t* didx;           // [frames][M]
+  float* slow_mag;         // [frames][C]
+  int64_t probe_frame;     // frame within this launch, -1 = none
+  int probe_chirp;
+  float* probe_mag;        // [NR]
+};
+
+struct StftArgs {
+  const float* slow_mag;   // [*][pn]
+  const int32_t* frame_list;
+  const int64_t* len;      // device scalar L
+  int pn;
+  const float* halo;
+  int n_halo;
+  const int64_t* halo_len;  // device, or nullptr -> n_halo
+  const float* win;        // device [wlen]
+  int wlen, hop, nfft;
+  float inv_fs;            // 1/fs; the 'psd' scale 1/(fs*sum(win^2)) is formed in-kernel
+  int64_t max_seg;
+  float* P;                // [max_seg][nfft/2+1]
+  float* pmax;
+  int64_t* nseg_out;
+};
+
+struct StftDbArgs {
+  const float* P;
+  const int64_t* nseg;
+  int64_t max_seg;
+  int nbins_in;            // nfft/2+1
+  const float* pmax;
+  int nlog;                // 0 = no resampling
+  const int32_t* lidx;     // [nlog]
+  const float* lw;         // [nlog]
+  float* out;
+};
+
+struct SynthArgs {
+  void* iq;
+  int dtype;
+  int64_t frame0, nframes;
+  int C, S, NR, ND;
+  float dist_per_bin;
+  const float2* cal;
+};
+
+hipError_t launch_range(const RangeArgs& a, hipStream_t s);
+hipError_t launch_doppler(const DopplerArgs& a, hipStream_t s);
+hipError_t launch_detect(const DetectArgs& a, hipStream_t s);
+hipError_t launch_compact(const int32_t* count, int64_t F, int pn, int32_t* frame_list, int64_t* len,
+                          hipStream_t s);
+hipError_t launch_stft_power(const StftArgs& a, hipStream_t s);
+hipError_t launch_stft_db(const StftDbArgs& a, hipStream_t s);
+hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
+hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s);
+
+bool range_size_supported(int nr);
+bool doppler_size_supported(int nd);
+
+}  // namespace fmcw

@@ -1,0 +1,266 @@
+// kernels_stft.hip -- slow-time compaction, STFT, dB/log-frequency stages and
+// the synthetic IQ generator.
+//
+//   k_compact     radar_processing.m:257-260  (which frames feed slow_time_signal)
+//   k_stft_power  :270-276  spectrogram(|slow|, win, noverlap, nfft, 1/PRT):
+//                 one-sided PSD P of every hop-spaced, window-long segment,
+//                 zero-padded to nfft, plus the running max of P
+//   k_stft_db     :279-283 psd = 20*log10(P/max(P(:)))  and  :293-299
+//                 interp1 onto 1024 logspace bins (table from the host)
+//   k_synth       SURVEY.md 8d synthetic frames (bench/test input only)
+#include "fft_team.h"
+#include "fmcw_internal.h"
+#include "../../include/fmcw.h"
+
+namespace fmcw {
+
+// ---------------------------------------------------------------------------
+// exclusive scan of (count > 0) over F frames in one 1024-thread workgroup
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_compact(const int32_t* __restrict__ count, int64_t F, int pn,
+                                                  int32_t* __restrict__ list, int64_t* __restrict__ len) {
+  __shared__ int wsum[16];
+  __shared__ long long carry;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < F; base += 1024) {
+    const int64_t i = base + tid;
+    const bool flag = i < F && count[i] > 0;
+    const unsigned long long bal = __ballot(flag);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) wsum[wid] = __popcll(bal);
+    __syncthreads();
+    int wpre = 0;
+    for (int q = 0; q < wid; ++q) wpre += wsum[q];
+    if (flag) list[carry + wpre + pre] = (int32_t)i;
+    __syncthreads();
+    if (tid == 0) {
+      int tot = 0;
+      for (int q = 0; q < 16; ++q) tot += wsum[q];
+      carry += tot;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *len = (int64_t)carry * pn;
+}
+
+// ---------------------------------------------------------------------------
+// STFT power.  A workgroup owns `seg_tile` consecutive segments; it stages the
+// samples they cover (through the compaction indirection) in LDS, then each
+// thread evaluates S(seg, bin) = sum_m x[seg*hop+m] w[m] e^{-2 pi i bin m/nfft}
+// by Horner's rule in z = e^{-2 pi i bin/nfft} (wlen-1 complex FMAs).
+// ---------------------------------------------------------------------------
+constexpr int STFT_MAX_SAMPLES = 8192;
+constexpr int STFT_MAX_WLEN = 256;
+
+__global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
+  __shared__ float xs[STFT_MAX_SAMPLES];
+  __shared__ float ws[STFT_MAX_WLEN];
+  __shared__ float bmax[4];
+  __shared__ float wss;
+  const int64_t L = *a.len;
+  const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
+  const int64_t Lx = L + H;
+  const int noverlap = a.wlen - a.hop;
+  int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
+  if (nseg > a.max_seg) nseg = a.max_seg;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+  const int64_t s0 = (int64_t)blockIdx.x * seg_tile;
+  if (s0 >= nseg) return;                                           // block-uniform
+  const int64_t s1 = (s0 + seg_tile < nseg) ? s0 + seg_tile : nseg;
+  const int nsamp = (int)((s1 - 1 - s0) * a.hop + a.wlen);
+  const int64_t q0 = s0 * a.hop;
+  for (int i = threadIdx.x; i < nsamp; i += 256) {
+    const int64_t q = q0 + i;
+    float x;
+    if (q < L) {
+      const int64_t fr = a.frame_list[q / a.pn];
+      x = a.slow_mag[fr * a.pn + (q % a.pn)];
+    } else {
+      x = a.halo[q - L];
+    }
+    xs[i] = x;
+  }
+  for (int i = threadIdx.x; i < a.wlen; i += 256) ws[i] = a.win[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float u = 0.f;
+    for (int i = 0; i < a.wlen; ++i) u = fmaf(ws[i], ws[i], u);
+    wss = a.inv_fs / u;                                             // 1/(fs*sum(w.^2))
+  }
+  __syncthreads();
+  const float p_scale = wss;
+
+  const int nb = a.nfft / 2 + 1;
+  const int64_t total = (s1 - s0) * nb;
+  const float two_over_nfft = 2.0f / (float)a.nfft;
+  float lmax = 0.f;
+  for (int64_t o = threadIdx.x; o < total; o += 256) {
+    const int sl = (int)(o / nb), bin = (int)(o - (int64_t)sl * nb);
+    float sn, cs;
+    sincospif((float)bin * two_over_nfft, &sn, &cs);
+    const float2 z = make_float2(cs, -sn);
+    const float* xp = xs + sl * a.hop;
+    float2 acc = make_float2(xp[a.wlen - 1] * ws[a.wlen - 1], 0.f);
+    for (int m = a.wlen - 2; m >= 0; --m) {
+      acc = cmul(acc, z);
+      acc.x = fmaf(xp[m], ws[m], acc.x);
+    }
+    const float k = (bin == 0 || 2 * bin == a.nfft) ? 1.f : 2.f;  // one-sided 'psd'
+    const float p = cabs2(acc) * p_scale * k;
+    a.P[(s0 + sl) * nb + bin] = p;
+    lmax = fmaxf(lmax, p);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+  if ((threadIdx.x & 63) == 0) bmax[threadIdx.x >> 6] = lmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
+    atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+  }
+}
+
+__global__ __launch_bounds__(256) void k_stft_db(StftDbArgs a) {
+  const int64_t nseg = *a.nseg;
+  const float inv = 1.0f / *a.pmax;
+  const int nout = a.nlog > 0 ? a.nlog : a.nbins_in;
+  const int64_t total = nseg * nout;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int64_t s = o / nout;
+    const int j = (int)(o - s * nout);
+    const float* row = a.P + s * a.nbins_in;
+    if (a.nlog == 0) {
+      a.out[o] = 20.0f * log10f(row[j] * inv);                     // :283
+    } else {
+      const int i0 = a.lidx[j];
+      const float w = a.lw[j];
+      const float d0 = 20.0f * log10f(row[i0] * inv), d1 = 20.0f * log10f(row[i0 + 1] * inv);
+      a.out[o] = d0 + w * (d1 - d0);                               // :299 interp1 'linear','extrap'
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// synthetic frames; the same integer hash as oracle/oracle.py
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ unsigned long long hmix(unsigned long long seed, unsigned long long ctr) {
+  return splitmix64(seed * 0xD1342543DE82EF95ull + ctr);
+}
+__device__ __forceinline__ double u24(unsigned long long h, int sh) {
+  return ((double)((h >> sh) & 0xFFFFFFull) + 0.5) / 16777216.0;
+}
+
+template <typename TOut>
+__global__ __launch_bounds__(256) void k_synth(SynthArgs a) {
+  const int64_t per_frame = (int64_t)a.C * a.S;
+  const int64_t total = a.nframes * per_frame;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  TOut* out = static_cast<TOut*>(a.iq);
+  const double dpb = a.dist_per_bin;
+  const int rlo = (int)ceil(0.9 / dpb) + 2;
+  int rhi = (int)floor(25.0 / dpb) - 2;
+  if (rhi < rlo) rhi = rlo;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+    const int64_t fl = e / per_frame;
+    const int64_t rem = e - fl * per_frame;
+    const int k = (int)(rem / a.S), n = (int)(rem - (int64_t)k * a.S);
+    const unsigned long long seed = 0xF3C0ull ^ (unsigned long long)(a.frame0 + fl);
+    const double u0 = u24(hmix(seed, 0x1000), 40), u1 = u24(hmix(seed, 0x1001), 40);
+    const double u2 = u24(hmix(seed, 0x1002), 40), u3 = u24(hmix(seed, 0x1003), 40);
+    const double u4 = u24(hmix(seed, 0x1004), 40), u5 = u24(hmix(seed, 0x1005), 40);
+    const bool no_target = u0 < 0.10;
+    const double off = u1 < 0.25 ? 0.37 : 0.0;
+    int ri = (int)(u2 * (rhi - rlo + 1));
+    if (ri > rhi - rlo) ri = rhi - rlo;
+    const int r = rlo + ri;
+    int d = 0;
+    if (a.ND > 1) {
+      int di = (int)(u3 * (a.ND - 1));
+      if (di > a.ND - 2) di = a.ND - 2;
+      d = -a.ND / 2 + 1 + di;
+    }
+    const double A = no_target ? 0.0 : 0.02 + 0.18 * u4;
+    const int dm = ((d % a.ND) + a.ND) % a.ND;
+    double ph = (double)(((int64_t)n * r) % a.NR) / a.NR + (double)n * off / a.NR +
+                (double)(((int64_t)k * dm) % a.ND) / a.ND + u5;
+    ph = ph - floor(ph);
+    float sn, cs;
+    sincospif((float)(2.0 * ph), &sn, &cs);
+    const unsigned long long h = hmix(seed, (unsigned long long)(k * (int64_t)a.S + n) + (1ull << 40));
+    const float v1 = (float)u24(h, 40), v2 = (float)u24(h, 16);
+    const float rad = sqrtf(-2.0f * logf(v1)) * (1e-3f * 0.70710678118654752f);
+    float ns, nc;
+    sincospif(2.0f * v2, &ns, &nc);
+    const float2 c = a.cal[n];
+    const float2 x = make_float2(c.x + (float)A * cs + rad * nc, c.y + (float)A * sn + rad * ns);
+    st_c(out, e, x);
+  }
+}
+
+__global__ void k_fill_u32(uint32_t* p, uint32_t v, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+
+static unsigned grid_for(int64_t n, int per_thread = 1) {
+  int64_t b = (n + 256LL * per_thread - 1) / (256LL * per_thread);
+  if (b < 1) b = 1;
+  if (b > 65536) b = 65536;
+  return (unsigned)b;
+}
+
+hipError_t launch_compact(const int32_t* count, int64_t F, int pn, int32_t* list, int64_t* len, hipStream_t s) {
+  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, count, F, pn, list, len);
+  return hipGetLastError();
+}
+
+hipError_t launch_stft_power(const StftArgs& a, hipStream_t s) {
+  if (a.max_seg <= 0) return hipSuccess;
+  if (a.wlen > STFT_MAX_WLEN || a.hop < 1) return hipErrorInvalidValue;
+  const int nb = a.nfft / 2 + 1;
+  int seg_tile = 4096 / nb;
+  if (seg_tile < 1) seg_tile = 1;
+  const int cap = (STFT_MAX_SAMPLES - a.wlen) / a.hop + 1;
+  if (seg_tile > cap) seg_tile = cap;
+  if (seg_tile > 1024) seg_tile = 1024;
+  const int64_t blocks = (a.max_seg + seg_tile - 1) / seg_tile;
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stft_power, dim3((unsigned)blocks), dim3(256), 0, s, a, seg_tile);
+  return hipGetLastError();
+}
+
+hipError_t launch_stft_db(const StftDbArgs& a, hipStream_t s) {
+  if (a.max_seg <= 0) return hipSuccess;
+  const int nout = a.nlog > 0 ? a.nlog : a.nbins_in;
+  hipLaunchKernelGGL(k_stft_db, dim3(grid_for(a.max_seg * nout, 4)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(const SynthArgs& a, hipStream_t s) {
+  const int64_t total = a.nframes * (int64_t)a.C * a.S;
+  if (total <= 0) return hipSuccess;
+  if (a.dtype == FMCW_C64)
+    hipLaunchKernelGGL((k_synth<float2>), dim3(grid_for(total, 4)), dim3(256), 0, s, a);
+  else if (a.dtype == FMCW_C32H)
+    hipLaunchKernelGGL((k_synth<__half2>), dim3(grid_for(total, 4)), dim3(256), 0, s, a);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_u32, dim3(grid_for(n, 4)), dim3(256), 0, s, p, v, n);
+  return hipGetLastError();
+}
+
+}  // namespace fmcw

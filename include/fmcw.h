@@ -1,0 +1,222 @@
+/*
+ * fmcw.h -- C-ABI of libfmcw, the MI355X (gfx950) FMCW radar DSP path.
+ *
+ * Drop-in boundary for the per-frame fast-time / slow-time / STFT loop of
+ * alepnabil/fmcw_radar_processing, radar-etl-pipeline/radar_processing.m
+ * (function radar_processing(process_animal_activity), :56).  The reference
+ * has no FFI layer of its own: every step is a MATLAB built-in call inside
+ * one serial loop.  The entry points below replace exactly these lines, and
+ * are what a MEX gateway (mex/fmcw_mex.c) binds; INTEGRATION.md shows the
+ * MATLAB-side call sequence and a ctypes binding.
+ *
+ *   fmcw_set_taps      <- :121/:136 IF_scale, :138-139 window taps, :166-174 calib_rx1
+ *   fmcw_process       <- :197-261 per-frame loop ('no' branch) + :265 range_tx1rx1_max_abs
+ *                         (:457-498 per-frame part of the 'yes' branch is the same math)
+ *   fmcw_range_fft     <- :203-205 + :207 + :210 only (range cube + profile; config 2)
+ *   fmcw_stft          <- :270-299 (|slow|, nextpow2, spectrogram, fftshift, 20log10,
+ *                         logspace + interp1)
+ *
+ * Conventions
+ *   - Plain C types only.  Complex data is interleaved (re, im) float32, which
+ *     is MATLAB's interleaved-complex `single` layout (-R2018a API).
+ *   - Array shapes are written C-style, last index fastest.  Every one of them
+ *     is also the memory layout of the MATLAB array named next to it, so a MEX
+ *     gateway hands MATLAB buffers through without copies or transposes.
+ *   - Return value: FMCW_OK (0) or a negative fmcw_status; the message of the
+ *     last failure on the calling thread is in fmcw_last_error().
+ *   - A context is NOT thread-safe: one per host thread (MEX keeps one static).
+ *   - The caller owns every I/O buffer; the library never returns memory.
+ *   - There is no CPU fallback: on a host without a usable gfx950 device
+ *     fmcw_ctx_create fails with FMCW_E_HIP.
+ */
+#ifndef FMCW_H_
+#define FMCW_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FMCW_ABI_VERSION 1
+
+typedef enum fmcw_status {
+  FMCW_OK = 0,
+  FMCW_E_ARG = -1,          /* bad argument / unsupported size                */
+  FMCW_E_HIP = -2,          /* HIP runtime failure (no device, launch, copy)   */
+  FMCW_E_OOM = -3,          /* device allocation failed                        */
+  FMCW_E_STATE = -4,        /* call order (e.g. fmcw_set_taps not called)      */
+  FMCW_E_DATA = -5          /* data-dependent failure MATLAB would raise, e.g.
+                               spectrogram of a signal shorter than the window */
+} fmcw_status;
+
+/* Element type of IQ input and of complex outputs. */
+typedef enum fmcw_dtype {
+  FMCW_C64 = 0,             /* complex float32, 8 B per sample                 */
+  FMCW_C32H = 1             /* complex float16, 4 B per sample (storage only;
+                               all arithmetic is float32).  fp16 OUTPUTS hold
+                               MATLAB's values divided by the FFT sizes applied
+                               so far (exact powers of two, to stay inside the
+                               fp16 range): range cube X/nr, RD map D/(nr*nd) */
+} fmcw_dtype;
+
+/* Algorithm parameters: radar_processing.m:117-154 (a1 in SURVEY.md 8a). */
+typedef struct fmcw_params {
+  int32_t nts;                  /* NTS, ADC samples per chirp            :109 */
+  int32_t pn;                   /* PN, chirps per frame                  :112 */
+  int32_t nr;                   /* range_fft_size (power of 2, 16..2048) :118 */
+  int32_t nd;                   /* Doppler_fft_size (power of 2, 2..1024):119 */
+  int32_t max_targets;          /* max_num_targets (1..8)                :129 */
+  int32_t doppler_fallback_idx; /* 1-based; the literal 9 of :234 in parity
+                                   mode, nd/2+1 in throughput mode            */
+  float if_scale;               /* IF_scale                          :121/136 */
+  float range_thr;              /* range_threshold                       :123 */
+  float doppler_thr;            /* Doppler_threshold                     :124 */
+  float min_d;                  /* min_distance [m]                      :126 */
+  float max_d;                  /* max_distance [m]                      :127 */
+  float dist_per_bin;           /* dist_per_bin [m]                      :147 */
+} fmcw_params;
+
+typedef struct fmcw_ctx fmcw_ctx;
+
+int32_t     fmcw_abi_version(void);
+const char* fmcw_last_error(void);
+int         fmcw_device_count(int32_t* n);
+
+/* Bind a context to HIP device `device_id` (one stream, scratch, tables). */
+int fmcw_ctx_create(int32_t device_id, fmcw_ctx** out);
+int fmcw_ctx_destroy(fmcw_ctx* ctx);
+
+/* Window taps and calibration (radar_processing.m:138, :139, :174):
+ *   range_win   [nts]        = 2*blackman(NTS)
+ *   doppler_win [pn]         = 2*chebwin(PN)
+ *   calib       [nts] c64    = calib_rx1
+ * Also builds the twiddle tables for nr and nd.  Must precede processing and
+ * be repeated whenever nts/pn/nr/nd change. */
+int fmcw_set_taps(fmcw_ctx* ctx, const fmcw_params* p, const float* range_win,
+                  const float* doppler_win, const float* calib);
+
+/* ---------------------------------------------------------------------------
+ * Host-pointer API (MEX / ctypes).  Data are staged through device memory
+ * owned by the context; the call returns when the outputs are on the host.
+ * ------------------------------------------------------------------------- */
+
+/* Per-frame stages a5-a11 + a13 of SURVEY 8a over F frames
+ * (radar_processing.m:199-239, :257-259, :265).
+ *   iq              [F][pn][nts]  in_dtype   cat(3, frame.Chirp(:,:,1))
+ *   range_profile   [F][nr]  f32   range_tx1rx1_max_abs (:265, Nr x F)
+ *   tgt_count       [F]      i32   num_of_targets (:213)
+ *   tgt_range_idx   [F][M]   i32   tgt_range_idx, 1-based, 0 where j >= count
+ *   tgt_range_mag   [F][M]   f32   tgt_range_mag
+ *   tgt_doppler_idx [F][M]   i32   tgt_doppler_idx (:227-239), 1-based
+ *   slow_mag        [F][pn]  f32   abs(range_tx1rx1_complete(ridx(1),:,fr)),
+ *                                  the slow-time samples appended at :259 and
+ *                                  made real at :270; zero where count == 0
+ *   range_cube      [F][pn][nr] c64 or NULL   range_tx1rx1_complete (:207)
+ *   rd_map          [F][nr][nd] c64 or NULL   range_Doppler_tx1rx1 (:219) for
+ *                                  EVERY range row (the reference fills only the
+ *                                  target rows; each row is the same row op).
+ *                                  Note the per-frame transpose vs MATLAB's Nr x Nd.
+ *   probe_column    1-based linear column of the Nr x (pn*F) view of the cube
+ *                   (:410-411 uses 100), 0 = none
+ *   probe_mag       [nr] f32 or NULL  abs(range_tx1rx1_complete(:, probe_column))
+ */
+int fmcw_process(fmcw_ctx* ctx, const fmcw_params* p, const void* iq, int32_t in_dtype,
+                 int64_t F, float* range_profile, int32_t* tgt_count, int32_t* tgt_range_idx,
+                 float* tgt_range_mag, int32_t* tgt_doppler_idx, float* slow_mag,
+                 float* range_cube, float* rd_map, int64_t probe_column, float* probe_mag);
+
+/* Range stage only (config 2): :203-205, :207, :210 -> cube + profile. */
+int fmcw_range_fft(fmcw_ctx* ctx, const fmcw_params* p, const void* iq, int32_t in_dtype,
+                   int64_t F, float* range_cube, float* range_profile);
+
+/* STFT + dB + optional log-frequency resampling (:270-299).
+ *   x [L] f32        iq_data = abs(slow_time_signal_all_frames)
+ *   win [wlen]       kaiser(20,3) (:276) in parity mode
+ *   noverlap         19 (:179); hop = wlen - noverlap
+ *   nfft             0 = the reference rule 2^nextpow2(L) (:273)
+ *   fs               1/PRT
+ *   n_log_bins       1024 (:293) -> intensity is interp1 onto logspace bins;
+ *                    0 -> intensity is 20log10(P/max P) on the nfft/2+1 bins
+ *   out: T [nseg], freq [n_log_bins or nfft/2+1], intensity [nseg][nbins_out]
+ *        (MATLAB's nbins_out x nseg matrix), nseg = fix((L-noverlap)/hop)
+ *   Query sizes first with fmcw_stft_sizes.  Fails with FMCW_E_DATA when
+ *   nseg < 1 (MATLAB's spectrogram raises on such input). */
+int fmcw_stft_sizes(int64_t L, int32_t wlen, int32_t noverlap, int32_t nfft,
+                    int32_t n_log_bins, int64_t* nseg, int32_t* nfft_used, int32_t* nbins_out);
+int fmcw_stft(fmcw_ctx* ctx, const float* x, int64_t L, const float* win, int32_t wlen,
+              int32_t noverlap, int32_t nfft, double fs, int32_t n_log_bins, float* T,
+              float* freq, float* intensity);
+
+/* ---------------------------------------------------------------------------
+ * Device-pointer API (benches, multi-GPU driver).  All pointers are device
+ * pointers on the context's device; `stream` is a hipStream_t (NULL = the
+ * context's own stream).  Calls are asynchronous on that stream.
+ * ------------------------------------------------------------------------- */
+int fmcw_process_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, int32_t in_dtype,
+                        int64_t F, float* d_range_profile, int32_t* d_tgt_count,
+                        int32_t* d_tgt_range_idx, float* d_tgt_range_mag,
+                        int32_t* d_tgt_doppler_idx, float* d_slow_mag, void* d_range_cube,
+                        void* d_rd_map, int32_t out_dtype, int64_t probe_column,
+                        float* d_probe_mag, void* stream);
+
+int fmcw_range_fft_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, int32_t in_dtype,
+                          int64_t F, void* d_range_cube, int32_t out_dtype, float* d_range_profile,
+                          void* stream);
+
+/* Slow-time compaction (:257-260): exclusive scan of (tgt_count>0) over F
+ * frames.  Writes d_frame_list[i] = i-th frame with a target, *d_len = L
+ * (= pn * #frames with a target, int64, device). */
+int fmcw_compact_device(fmcw_ctx* ctx, const int32_t* d_tgt_count, int64_t F, int32_t pn,
+                        int32_t* d_frame_list, int64_t* d_len, void* stream);
+
+/* Power spectrogram of the compacted |slow| signal, segments [0, nseg) with
+ * nseg = fix((L + H - noverlap)/hop) clipped to max_seg (all on device):
+ * sample q < L is slow_mag[frame_list[q/pn]][q%pn], q >= L is d_halo[q-L].
+ * H = *d_halo_len when d_halo_len != NULL (device int64, <= n_halo), else
+ * n_halo.  The halo carries the first samples of the following shards in the
+ * multi-GPU split of the concatenated slow-time signal (:259).
+ *   d_P [max_seg][nfft/2+1]  MATLAB P (psd scaling, one-sided)
+ *   d_pmax                   running max of P (float, atomically raised;
+ *                            initialise to 0 before the first call)
+ *   d_nseg                   int64 device: segments actually written */
+int fmcw_stft_power_device(fmcw_ctx* ctx, const float* d_slow_mag, const int32_t* d_frame_list,
+                           const int64_t* d_len, int32_t pn, const float* d_halo, int32_t n_halo,
+                           const int64_t* d_halo_len, const float* d_win, int32_t wlen, int32_t noverlap, int32_t nfft,
+                           double fs, int64_t max_seg, float* d_P, float* d_pmax,
+                           int64_t* d_nseg, void* stream);
+
+/* psd = 20*log10(P / pmax) (:282-283), optionally resampled onto n_log_bins
+ * logspace bins (:293-299).  d_out [max_seg][n_log_bins or nfft/2+1]; may
+ * alias d_P when n_log_bins == 0. */
+int fmcw_stft_db_device(fmcw_ctx* ctx, const float* d_P, const int64_t* d_nseg, int64_t max_seg,
+                        int32_t nfft, double fs, const float* d_pmax, int32_t n_log_bins,
+                        float* d_out, void* stream);
+
+/* Synthetic IQ frames of SURVEY 8d (seed 0xF3C0 ^ global frame index),
+ * generated in place in HBM: d_iq [F][pn][nts] of dtype.  Bench input only. */
+int fmcw_synth_device(fmcw_ctx* ctx, const fmcw_params* p, int64_t frame0, int64_t F,
+                      void* d_iq, int32_t dtype, void* stream);
+
+/* Per-stage device timing with HIP events on the launching streams.
+ * enable: 0 off; 1 = the range+Doppler span of each fmcw_process_device call
+ * (stage 7: event before the first range launch .. event after the last
+ * Doppler launch; the chunks run as a 3-stream software pipeline) and one pair
+ * per STFT-side launch (stages 3-6); 2 = additionally one pair per K1/K2/K3.
+ * stage: 0 range, 1 doppler, 2 detect, 3 compact, 4 stft_power, 5 stft_db,
+ *        6 range_only, 7 range+Doppler span.  fmcw_timing_read synchronises. */
+int fmcw_timing_enable(fmcw_ctx* ctx, int32_t enable);
+int fmcw_timing_read(fmcw_ctx* ctx, int32_t stage, double* total_ms, int64_t* launches);
+int fmcw_timing_reset(fmcw_ctx* ctx);
+
+/* Frames per range/Doppler chunk (the range cube of one chunk is the only
+ * intermediate; it is sized to stay in the 256 MiB Infinity Cache).
+ * 0 restores the default. */
+int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
+
+int fmcw_synchronize(fmcw_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FMCW_H_ */

@@ -1,0 +1,194 @@
+"""GPU parity: libfmcw (HIP, gfx950) vs the float64 oracle on the same inputs.
+
+Every comparison goes through the C-ABI (Engine -> libfmcw.so).  Tolerances
+are those of SURVEY.md 8d and are written next to each assertion.
+"""
+import numpy as np
+import pytest
+
+from fmcw_radar_processing_amd import FMCW_C32H, FMCW_C64
+from fmcw_radar_processing_amd import params as P
+from oracle import oracle as O
+from tests.helpers import (TOL_FP16_DB, TOL_FP16_REL_L2, TOL_FP32_DB, TOL_FP32_REL_L2, case,
+                           near_tie_frames, rd_rel_err, rel_l2)
+
+pytestmark = pytest.mark.gpu
+
+GEOMS = [
+    # (nts, pn, nr, nd, F, mode)            what it exercises
+    (64, 16, 256, 16, 12, P.PARITY),        # deployed module: zero-pad 64 -> 256, literal 9 fallback
+    (256, 128, 256, 16, 3, P.PARITY),       # config 1: Doppler truncation (Nd 16 < PN 128)
+    (512, 128, 512, 16, 4, P.THROUGHPUT),   # config 2 geometry
+    (1024, 256, 1024, 256, 3, P.THROUGHPUT),  # config 3/4 geometry
+    (100, 20, 128, 32, 5, P.PARITY),        # ragged: NTS, PN not powers of two; Nd > PN (zero pad)
+    (300, 8, 256, 4, 4, P.PARITY),          # NTS > Nr (fft truncates; the mean keeps all samples)
+    (1024, 64, 2048, 64, 2, P.THROUGHPUT),  # two-wave range team (Nr 2048)
+]
+
+
+def _run(engine, nts, pn, nr, nd, F, mode, frame0=0):
+    cfg, p, wr, wd, cal = case(nts, pn, nr, nd, mode)
+    iq = O.synth_frames(F, pn, nts, nr, nd, p["dist_per_bin"], frame0=frame0)
+    engine.set_taps(cfg, cal, wr, wd)
+    got = engine.process(iq, want_cube=True, want_rd=True, probe_column=min(100, F * pn))
+    ref = O.process_frames(iq, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
+    return cfg, p, iq, got, ref
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=[f"{g[0]}x{g[1]}_nr{g[2]}_nd{g[3]}" for g in GEOMS])
+def test_process_matches_oracle(engine, geom):
+    cfg, p, iq, got, ref = _run(engine, *geom)
+    F = iq.shape[0]
+    wd = O.windows(cfg.nts, cfg.pn)[1]
+    # fp32: per-frame relative L2 of the range cube and the RD map <= 1e-5
+    # (RD normalisation: see helpers.rd_rel_err -- static-target cancellation)
+    assert rel_l2(got["cube"], ref["cube"], axis=(1, 2)).max() <= TOL_FP32_REL_L2
+    assert rd_rel_err(got["rd"], ref["rd"], ref["cube"], wd, cfg.nd).max() <= TOL_FP32_REL_L2
+    assert rel_l2(got["profile"], ref["profile"], axis=1).max() <= TOL_FP32_REL_L2
+    # detections: exact except near-ties
+    ok = ~near_tie_frames(ref["profile"])
+    np.testing.assert_array_equal(got["tgt_count"][ok], ref["tgt_count"][ok])
+    np.testing.assert_array_equal(got["tgt_range_idx"][ok], ref["tgt_range_idx"][ok])
+    np.testing.assert_array_equal(got["tgt_doppler_idx"][ok], ref["tgt_doppler_idx"][ok])
+    np.testing.assert_allclose(got["tgt_range_mag"], ref["tgt_range_mag"], rtol=1e-5, atol=0)
+    has = ref["tgt_count"] > 0
+    if has.any():
+        assert rel_l2(got["slow_mag"][has], ref["slow_mag"][has], axis=1).max() <= TOL_FP32_REL_L2
+    assert np.all(got["slow_mag"][~has] == 0)
+    # probe column (:410-411): linear column of the Nr x (PN*F) cube
+    col = min(100, F * cfg.pn) - 1
+    want = np.abs(ref["cube"][col // cfg.pn, col % cfg.pn, :])
+    assert rel_l2(got["probe_mag"], want) <= TOL_FP32_REL_L2
+
+
+def test_detections_are_the_planted_targets(engine):
+    """Known answer: integer-bin range tone r lands at idx r+1, Doppler tone d at d+Nd/2+1."""
+    cfg, p, iq, got, ref = _run(engine, 1024, 256, 1024, 256, 8, P.THROUGHPUT, frame0=40)
+    for i in range(iq.shape[0]):
+        fp = O.synth_frame_params(40 + i, 1024, 256, p["dist_per_bin"])
+        if fp["A"] == 0:
+            assert got["tgt_count"][i] == 0
+            continue
+        assert got["tgt_range_idx"][i, 0] == fp["r"] + 1
+        if fp["d"] == 0:
+            assert got["tgt_doppler_idx"][i, 0] == cfg.doppler_fallback_idx
+        else:
+            assert got["tgt_doppler_idx"][i, 0] == fp["d"] + 128 + 1
+
+
+def test_multi_target(engine):
+    cfg, p, wr, wd, cal = case(256, 32, 256, 32, P.PARITY)
+    cfg.max_targets = 3
+    p["max_targets"] = 3
+    F = 6
+    iq = O.synth_frames(F, 32, 256, 256, 32, p["dist_per_bin"])
+    n = np.arange(256)
+    # add two more tones per frame at distinct bins
+    for f in range(F):
+        for rr, a in ((12 + f, 0.05), (20 + 2 * f, 0.08)):
+            iq[f] += (a * np.exp(2j * np.pi * n * rr / 256))[None, :].astype(np.complex64)
+    engine.set_taps(cfg, cal, wr, wd)
+    got = engine.process(iq)
+    ref = O.process_frames(iq, cal, p, wr, wd)
+    np.testing.assert_array_equal(got["tgt_count"], ref["tgt_count"])
+    np.testing.assert_array_equal(got["tgt_range_idx"], ref["tgt_range_idx"])
+    np.testing.assert_array_equal(got["tgt_doppler_idx"], ref["tgt_doppler_idx"])
+
+
+def test_chunking_is_invisible(engine):
+    """The per-chunk scratch cube must not change results (chunk 1 vs default)."""
+    cfg, p, wr, wd, cal = case(512, 64, 512, 64, P.THROUGHPUT)
+    iq = O.synth_frames(7, 64, 512, 512, 64, p["dist_per_bin"])
+    engine.set_taps(cfg, cal, wr, wd)
+    a = engine.process(iq)
+    engine.set_chunk_frames(2)
+    b = engine.process(iq)
+    engine.set_chunk_frames(0)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_range_fft_only(engine):
+    cfg, p, wr, wd, cal = case(512, 128, 512, 16, P.THROUGHPUT)
+    iq = O.synth_frames(3, 128, 512, 512, 16, p["dist_per_bin"])
+    engine.set_taps(cfg, cal, wr, wd)
+    cube, prof = engine.range_fft(iq)
+    ref = O.process_frames(iq, cal, p, wr, wd, want_cube=True)
+    assert rel_l2(cube, ref["cube"], axis=(1, 2)).max() <= TOL_FP32_REL_L2
+    assert rel_l2(prof, ref["profile"], axis=1).max() <= TOL_FP32_REL_L2
+
+
+def test_deterministic(engine):
+    cfg, p, wr, wd, cal = case(1024, 256, 1024, 256, P.THROUGHPUT)
+    iq = O.synth_frames(2, 256, 1024, 1024, 256, p["dist_per_bin"])
+    engine.set_taps(cfg, cal, wr, wd)
+    a = engine.process(iq, want_rd=True)
+    b = engine.process(iq, want_rd=True)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+@pytest.mark.parametrize("L,nfft,nlog", [(19 * 16 + 1, 0, 1024), (16 * 115, 0, 1024), (2000, 64, 0), (500, 0, 0)])
+def test_stft_matches_oracle(engine, L, nfft, nlog):
+    rng = np.random.default_rng(L)
+    x = np.abs(rng.standard_normal(L) + 3 * np.sin(np.arange(L) * 0.3)).astype(np.float32).astype(np.float64)
+    win = O.stft_window("kaiser") if nfft == 0 else O.stft_window("hann")
+    prt = 8e-4
+    got = engine.stft(x, win, 19, 1 / prt, nfft=nfft, n_log_bins=nlog)
+    ref = O.spectrogram_pipeline(x, prt, win, 19, nfft=nfft or None, nbins=nlog)
+    assert got["nfft"] == ref["nfft"]
+    np.testing.assert_allclose(got["time"], ref["time"], rtol=1e-6)
+    np.testing.assert_allclose(got["frequency"], ref["frequency"], rtol=1e-6)
+    ri = ref["intensity"].T if nlog else ref["intensity"].T   # oracle is bins x nseg
+    gi = got["intensity"]
+    assert gi.shape == ri.shape
+    sel = ri > -80
+    # fp32: |dB error| <= 1e-3 where psd > -80 dB
+    assert np.abs(gi[sel] - ri[sel]).max() <= TOL_FP32_DB
+
+
+def test_stft_rejects_short_signal(engine):
+    from fmcw_radar_processing_amd import FmcwError
+    with pytest.raises(FmcwError, match="E_DATA"):
+        engine.stft(np.ones(10), O.stft_window("kaiser"), 19, 1250.0)
+
+
+def test_synth_generator_matches_oracle(engine):
+    import torch
+    cfg, p, wr, wd, cal = case(256, 32, 256, 32, P.THROUGHPUT)
+    engine.set_taps(cfg, cal, wr, wd)
+    F = 5
+    d = torch.empty((F, 32, 256, 2), dtype=torch.float32, device="cuda")
+    engine.synth_device(d, 3, F, FMCW_C64)
+    torch.cuda.synchronize()
+    got = d.cpu().numpy().view(np.complex64)[..., 0]
+    ref = O.synth_frames(F, 32, 256, 256, 32, p["dist_per_bin"], frame0=3)
+    assert np.abs(got - ref).max() < 2e-6
+
+
+def test_fp16_storage_tolerance(engine):
+    """Config 4 fp16 storage: fp16 IQ in, fp16 RD out, fp32 arithmetic."""
+    import torch
+    cfg, p, wr, wd, cal = case(1024, 256, 1024, 256, P.THROUGHPUT)
+    engine.set_taps(cfg, cal, wr, wd)
+    F = 3
+    iq = O.synth_frames(F, 256, 1024, 1024, 256, p["dist_per_bin"])
+    iq16 = np.stack([iq.real, iq.imag], -1).astype(np.float16)
+    d_iq = torch.from_numpy(iq16).cuda()
+    outs = dict(profile=torch.empty((F, 1024), device="cuda"), tgt_count=torch.empty(F, dtype=torch.int32, device="cuda"),
+                tgt_range_idx=torch.empty((F, 1), dtype=torch.int32, device="cuda"),
+                tgt_range_mag=torch.empty((F, 1), device="cuda"),
+                tgt_doppler_idx=torch.empty((F, 1), dtype=torch.int32, device="cuda"),
+                slow_mag=torch.empty((F, 256), device="cuda"))
+    d_rd = torch.empty((F, 1024, 256, 2), dtype=torch.float16, device="cuda")
+    engine.process_device(d_iq, F, FMCW_C32H, outs, d_rd=d_rd, out_dtype=FMCW_C32H,
+                          stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    # fp16 outputs hold D / (Nr*Nd) (include/fmcw.h, FMCW_C32H)
+    rd = d_rd.float().cpu().numpy().view(np.complex64)[..., 0].astype(np.complex128) * (1024 * 256)
+    ref = O.process_frames(iq16.astype(np.float32).view(np.complex64)[..., 0], cal, p, wr, wd, want_rd=True,
+                           rd_all_rows=True)
+    ref_c = O.process_frames(iq16.astype(np.float32).view(np.complex64)[..., 0], cal, p, wr, wd, want_cube=True)
+    err = rd_rel_err(rd, ref["rd"], ref_c["cube"], wd, 256)
+    assert err.max() <= TOL_FP16_REL_L2, err
+    np.testing.assert_array_equal(outs["tgt_range_idx"].cpu().numpy(), ref["tgt_range_idx"])
