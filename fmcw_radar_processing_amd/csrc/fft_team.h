@@ -38,6 +38,43 @@ __device__ __forceinline__ float2 ld_c(const __half2* p, int64_t i) { return __h
 __device__ __forceinline__ void st_c(float2* p, int64_t i, float2 v) { p[i] = v; }
 __device__ __forceinline__ void st_c(__half2* p, int64_t i, float2 v) { p[i] = __float22half2_rn(v); }
 
+// Two adjacent complex elements in one 16-byte (c64) / 8-byte (c32h) access.
+__device__ __forceinline__ void ld_c2(const float2* p, int64_t i, float2& a, float2& b) {
+  const float4 v = *reinterpret_cast<const float4*>(p + i);
+  a = make_float2(v.x, v.y);
+  b = make_float2(v.z, v.w);
+}
+__device__ __forceinline__ void ld_c2(const __half2* p, int64_t i, float2& a, float2& b) {
+  const uint2 v = *reinterpret_cast<const uint2*>(p + i);
+  a = __half22float2(*reinterpret_cast<const __half2*>(&v.x));
+  b = __half22float2(*reinterpret_cast<const __half2*>(&v.y));
+}
+__device__ __forceinline__ void st_c2(float2* p, int64_t i, float2 a, float2 b) {
+  *reinterpret_cast<float4*>(p + i) = make_float4(a.x, a.y, b.x, b.y);
+}
+__device__ __forceinline__ void st_c2(__half2* p, int64_t i, float2 a, float2 b) {
+  const __half2 ha = __float22half2_rn(a), hb = __float22half2_rn(b);
+  uint2 v;
+  v.x = *reinterpret_cast<const unsigned*>(&ha);
+  v.y = *reinterpret_cast<const unsigned*>(&hb);
+  *reinterpret_cast<uint2*>(p + i) = v;
+}
+
+// Lane pair exchange (hardware lanes 2i <-> 2i+1, one DPP quad_perm [1,0,3,2]
+// per float, no LDS).  Each lane of a pair accessed two ADJACENT elements of
+// its own block (even lane: block A, odd lane: block B); afterwards the even
+// lane holds element 0 of blocks (A, B) and the odd lane element 1 of (A, B).
+// The same call turns the cyclic FFT layout back into adjacent pairs for
+// 16-byte stores.  Must be executed by both lanes of every pair.
+__device__ __forceinline__ float lane_swap1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ void pair_xchg(bool odd, float2& first, float2& second) {
+  const float2 send = odd ? first : second;
+  const float2 r = make_float2(lane_swap1(send.x), lane_swap1(send.y));
+  if (odd) first = r; else second = r;
+}
+
 // ---- small forward DFTs in registers (natural order in and out) -----------
 __device__ __forceinline__ void dft2(float2& a, float2& b) {
   const float2 t = a;
@@ -109,6 +146,9 @@ template <int N> struct FftPlan {
   static constexpr int P = N < 16 ? N : 16;   // values per thread
   static constexpr int T = N / P;             // threads per team
   static constexpr int LDS = (N < 16) ? 0 : N + N / 16;  // complex elements of LDS per team
+  // stride between the LDS regions of teams that share a wave: odd, so the same
+  // element of 16 neighbouring teams lands on 16 different bank pairs
+  static constexpr int STRIDE = (N < 16) ? 0 : (LDS | 1);
 };
 
 __device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }

@@ -212,10 +212,12 @@ int upload_twiddles(DevBuf& buf, int n, hipStream_t s) {
 }
 
 int64_t default_chunk(const fmcw_params* p) {
-  // The range cube of one chunk is the only intermediate: 64 MiB keeps it and
-  // the chunk's input/output streams inside the 256 MiB Infinity Cache.
+  // The range cube of one chunk is the only intermediate.  Measured on MI355X
+  // (tools/mall_probe.hip): re-reading a freshly written buffer is no faster
+  // from the Infinity Cache than from HBM, so the chunk is sized for launch
+  // efficiency (long kernels, few boundaries): 256 MiB per slot, 3 slots.
   const int64_t per_frame = (int64_t)p->pn * p->nr * 8;
-  int64_t c = (64ll << 20) / std::max<int64_t>(per_frame, 1);
+  int64_t c = (256ll << 20) / std::max<int64_t>(per_frame, 1);
   return std::max<int64_t>(c, 1);
 }
 

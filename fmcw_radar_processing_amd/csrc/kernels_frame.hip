@@ -54,12 +54,13 @@ __device__ __forceinline__ float2 team_sum(float2 s, float2* red, int t) {
 // consecutive chirps.  Thread t loads samples t + T*m (coalesced), keeps them
 // in registers through the FFT and stores range bins t + T*m (coalesced).
 // ---------------------------------------------------------------------------
-template <int NR, typename TIn, typename TCube, bool PROFILE>
+template <int NR, typename TIn, typename TCube, bool PROFILE, bool PAIR>
 __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
   using Plan = FftPlan<NR>;
   constexpr int P = Plan::P, T = Plan::T;
   constexpr int TEAMS = T >= 256 ? 1 : 256 / T;
-  constexpr int LDSN = Plan::LDS > 0 ? Plan::LDS : 1;
+  constexpr int LDSN = Plan::STRIDE > 0 ? Plan::STRIDE : 1;
+  static_assert(!PAIR || (T % 2 == 0 && P % 2 == 0), "pair access needs an even team");
   __shared__ float2 lds[TEAMS * LDSN];
   __shared__ float2 red[TEAMS * (T > 64 ? T / 64 : 1)];
 
@@ -86,16 +87,32 @@ __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
     // hoisting costs ~100 VGPRs and halves occupancy).
     int t = t0;
     asm volatile("" : "+v"(t));
+    const bool odd = (t & 1) != 0;
     const TIn* __restrict__ x = in + g * S;
     float2 v[P];
     float2 s = make_float2(0.f, 0.f);
+    if constexpr (PAIR) {
+      // 16-byte loads: lane pair (2i, 2i+1) reads samples 2i, 2i+1 of blocks
+      // 2j and 2j+1 (T samples each), then swaps one element (pair_xchg)
 #pragma unroll
-    for (int m = 0; m < P; ++m) {
-      const int n = t + T * m;
-      float2 xv = make_float2(0.f, 0.f);
-      if (valid && n < nmax) xv = ld_c(x, n);
-      v[m] = xv;
-      s = cadd(s, xv);
+      for (int j = 0; j < P / 2; ++j) {
+        const int e0 = T * (2 * j + (t & 1)) + 2 * (t >> 1);
+        float2 u0 = make_float2(0.f, 0.f), u1 = u0;
+        if (valid && e0 < nmax) ld_c2(x, e0, u0, u1);    // nmax even: e0+1 < nmax too
+        pair_xchg(odd, u0, u1);
+        v[2 * j] = u0;
+        v[2 * j + 1] = u1;
+        s = cadd(s, cadd(u0, u1));
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        const int n = t + T * m;
+        float2 xv = make_float2(0.f, 0.f);
+        if (valid && n < nmax) xv = ld_c(x, n);
+        v[m] = xv;
+        s = cadd(s, xv);
+      }
     }
     if (S > NR && valid) {                                     // samples beyond Nr still enter the mean
       for (int n = NR + t; n < S; n += T) s = cadd(s, ld_c(x, n));
@@ -116,14 +133,21 @@ __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
       }
     }
     team_fft<NR>(v, my, t, a.tw, Sync{});                     // :205 fft(., Nr, 1)
-    if (valid) {
-      TCube* __restrict__ o = out + g * NR;
-#pragma unroll
-      for (int m = 0; m < P; ++m) st_c(o, t + T * m, cscale(v[m], a.cube_scale));    // :207
-    }
     if constexpr (PROFILE) {
 #pragma unroll
       for (int m = 0; m < P; ++m) pm[m] = fmaxf(pm[m], cabs2(v[m]));
+    }
+    TCube* __restrict__ o = out + g * NR;
+    if constexpr (PAIR) {
+#pragma unroll
+      for (int j = 0; j < P / 2; ++j) {                        // :207, 16-byte stores
+        float2 p0 = cscale(v[2 * j], a.cube_scale), p1 = cscale(v[2 * j + 1], a.cube_scale);
+        pair_xchg(odd, p0, p1);
+        if (valid) st_c2(o, T * (2 * j + (t & 1)) + 2 * (t >> 1), p0, p1);
+      }
+    } else if (valid) {
+#pragma unroll
+      for (int m = 0; m < P; ++m) st_c(o, t + T * m, cscale(v[m], a.cube_scale));    // :207
     }
   }
   if constexpr (PROFILE) {
@@ -147,9 +171,11 @@ __global__ __launch_bounds__(256) void k_doppler(DopplerArgs a) {
   using Plan = FftPlan<ND>;
   constexpr int P = Plan::P, T = Plan::T;
   constexpr int RB = 256 / T;
-  constexpr int FFTL = RB * Plan::LDS, STGL = RB * (ND + 1);
+  constexpr int SROW = ND + 2;           // staging row: 16-byte aligned rows for float4 reads
+  constexpr int FFTL = RB * Plan::STRIDE, STGL = RB * SROW;
   constexpr int LDSN = FFTL > STGL ? FFTL : STGL;
-  __shared__ float2 lds[LDSN];
+  static_assert(RB % 2 == 0 && P % 2 == 0, "pair access needs even tiles");
+  __shared__ __attribute__((aligned(16))) float2 lds[LDSN];
   __shared__ float2 red_s[256];
   __shared__ float red_m[256];
 
@@ -159,20 +185,30 @@ __global__ __launch_bounds__(256) void k_doppler(DopplerArgs a) {
   const int b = threadIdx.x % RB, u = threadIdx.x / RB;
   const int r = tile * RB + b;
   const bool vb = r < NR;
+  const bool odd = (b & 1) != 0;         // = hardware lane parity (RB even)
   const TCube* __restrict__ cube = static_cast<const TCube*>(a.cube) + (int64_t)f * C * NR;
   const int kfft = C < ND ? C : ND;      // fft(., Nd, 2) truncates to the first Nd chirps
+  const int r2 = tile * RB + 2 * (b >> 1);
 
   float2 v[P];
   float2 s = make_float2(0.f, 0.f);
   float pm = 0.f;
+  // 16-byte loads: lane pair (2i, 2i+1) reads bins r2, r2+1 of chirps
+  // u + T*2j (even lane) and u + T*(2j+1) (odd lane), then swaps one element
 #pragma unroll
-  for (int m = 0; m < P; ++m) {
-    const int k = u + T * m;
-    float2 x = make_float2(0.f, 0.f);
-    if (vb && k < kfft) x = cscale(ld_c(cube, (int64_t)k * NR + r), a.cube_unscale);
-    v[m] = x;
-    s = cadd(s, x);
-    pm = fmaxf(pm, cabs2(x));
+  for (int j = 0; j < P / 2; ++j) {
+    const int k = u + T * (2 * j + (b & 1));
+    float2 u0 = make_float2(0.f, 0.f), u1 = u0;
+    if (r2 < NR && k < kfft) {
+      ld_c2(cube, (int64_t)k * NR + r2, u0, u1);
+      u0 = cscale(u0, a.cube_unscale);
+      u1 = cscale(u1, a.cube_unscale);
+    }
+    pair_xchg(odd, u0, u1);
+    v[2 * j] = u0;
+    v[2 * j + 1] = u1;
+    s = cadd(s, cadd(u0, u1));
+    pm = fmaxf(pm, fmaxf(cabs2(u0), cabs2(u1)));
   }
   if (C > ND && vb) {                    // chirps beyond Nd: profile and mean only
     for (int k = ND + u; k < C; k += T) {
@@ -200,19 +236,20 @@ __global__ __launch_bounds__(256) void k_doppler(DopplerArgs a) {
     const int k = u + T * m;
     v[m] = (k < kfft) ? cscale(csub(v[m], mean), a.wd[k]) : make_float2(0.f, 0.f);  // :218-219
   }
-  team_fft<ND>(v, lds + b * Plan::LDS, u, a.tw, BlockSync{}); // :219 fft(., Nd, 2)
+  team_fft<ND>(v, lds + b * Plan::STRIDE, u, a.tw, BlockSync{}); // :219 fft(., Nd, 2)
   __syncthreads();
 #pragma unroll
   for (int m = 0; m < P; ++m) {
     const int e = u + T * m;
-    lds[b * (ND + 1) + ((e + ND / 2) & (ND - 1))] = v[m];     // :219 fftshift(., 2)
+    lds[b * SROW + ((e + ND / 2) & (ND - 1))] = v[m];          // :219 fftshift(., 2)
   }
   __syncthreads();
   const int nrows = (NR - tile * RB) < RB ? (NR - tile * RB) : RB;
   TRd* __restrict__ out = static_cast<TRd*>(a.rd) + ((int64_t)f * NR + (int64_t)tile * RB) * ND;
-  for (int e = threadIdx.x; e < nrows * ND; e += 256) {
-    const int bb = e / ND, d = e & (ND - 1);
-    st_c(out, e, cscale(lds[bb * (ND + 1) + d], a.rd_scale));
+  for (int e2 = threadIdx.x; e2 < nrows * (ND / 2); e2 += 256) {   // RB whole rows, 16-byte stores
+    const int e = 2 * e2, bb = e / ND, d = e & (ND - 1);
+    const float4 q = *reinterpret_cast<const float4*>(&lds[bb * SROW + d]);
+    st_c2(out, e, cscale(make_float2(q.x, q.y), a.rd_scale), cscale(make_float2(q.z, q.w), a.rd_scale));
   }
 }
 
@@ -332,10 +369,16 @@ static hipError_t go_range(const RangeArgs& a, hipStream_t s) {
   constexpr int TEAMS = T >= 256 ? 1 : 256 / T;
   const int64_t per_block = (int64_t)TEAMS * a.cpt;
   const int64_t blocks = (a.nchirps + per_block - 1) / per_block;
-  if (a.profile)
-    hipLaunchKernelGGL((k_range<NR, TIn, TCube, true>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_range<NR, TIn, TCube, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  // 16-byte (pair) access needs an even team and 16-byte-aligned chirp rows
+  constexpr bool kPairOk = (T % 2 == 0);
+  const bool pair = kPairOk && (a.S % 2 == 0);
+  if (a.profile) {
+    if (pair) hipLaunchKernelGGL((k_range<NR, TIn, TCube, true, kPairOk>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_range<NR, TIn, TCube, true, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  } else {
+    if (pair) hipLaunchKernelGGL((k_range<NR, TIn, TCube, false, kPairOk>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((k_range<NR, TIn, TCube, false, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  }
   return hipGetLastError();
 }
 

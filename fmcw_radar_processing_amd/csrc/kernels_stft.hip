@@ -124,7 +124,8 @@ __global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
 
 __global__ __launch_bounds__(256) void k_stft_db(StftDbArgs a) {
   const int64_t nseg = *a.nseg;
-  const float inv = 1.0f / *a.pmax;
+  const float pm = *a.pmax;
+  const float inv = pm > 0.f ? 1.0f / pm : 0.f;   // all-zero P: 20log10(0) = -Inf, as MATLAB's G = 0 guard (:551)
   const int nout = a.nlog > 0 ? a.nlog : a.nbins_in;
   const int64_t total = nseg * nout;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;

@@ -76,15 +76,21 @@ def global_max_(pmax: torch.Tensor) -> torch.Tensor:
 
 
 def gather_range_speed(count: torch.Tensor, ridx: torch.Tensor, didx: torch.Tensor, rmag: torch.Tensor,
-                       dst: int = 0):
-    """range_speed concatenation (:386-389): per-frame (count, ridx, didx, mag) of
-    every rank on rank ``dst`` as one [world*F][3+...] float32 tensor (equal
-    shard sizes), else None on the other ranks."""
-    rows = torch.cat([count.reshape(-1, 1).float(), ridx.float(), didx.float(), rmag.float()], 1).contiguous()
-    world = dist.get_world_size()
-    if dist.get_rank() == dst:
+                       F_total: int | None = None, dst: int = 0):
+    """range_speed concatenation (:386-389): per-frame rows (count, ridx.., didx.., rmag..)
+    of every rank, in frame order, on rank ``dst`` as one float32 tensor; None on
+    the other ranks.  Shards may differ by one frame (shard_range): rows are
+    padded to ceil(F_total/world) for the collective and trimmed on ``dst``."""
+    rows = torch.cat([count.reshape(-1, 1).float(), ridx.float(), didx.float(), rmag.float()], 1)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    F_total = F_total if F_total is not None else rows.shape[0] * world
+    cap = -(-F_total // world)
+    if rows.shape[0] < cap:
+        rows = torch.cat([rows, rows.new_zeros(cap - rows.shape[0], rows.shape[1])], 0)
+    rows = rows.contiguous()
+    if rank == dst:
         bufs = [torch.empty_like(rows) for _ in range(world)]
         dist.gather(rows, gather_list=bufs, dst=dst)
-        return torch.cat(bufs, 0)
+        return torch.cat([b[: shard_range(F_total, r, world)[1]] for r, b in enumerate(bufs)], 0)
     dist.gather(rows, dst=dst)
     return None

@@ -1,0 +1,197 @@
+"""Host mirror of ``radar_processing(process_animal_activity)``
+(radar-etl-pipeline/radar_processing.m:56), with the loop and the STFT on the GPU.
+
+The MATLAB host keeps the same structure (see matlab/radar_processing.m and
+INTEGRATION.md); this module is the same sequence in Python so the path can be
+driven, tested and benchmarked without MATLAB:
+
+  :86       [frame, frame_count, calib_data, sXML] = f_parse_data2(...)  -> arguments
+            (f_parse_data2 is absent from the reference; the caller supplies the
+            parsed frames, calibration vector and device fields)
+  :89-174   params, windows, calibration                    -> params.py (host)
+  :197-261  per-frame loop                                   -> Engine.process (libfmcw)
+  :242-252  measurement update, incl. its (fr_idx, j) growth  -> measurement_update_no
+  :257-260  slow-time concatenation                          -> slow_time_signal
+  :265-299  max-abs profile, STFT, dB, log-frequency resample -> Engine.stft (libfmcw)
+  :302-436  four JSON files + uploads                        -> write_outputs_no
+  :440-607  'yes' branch: per-100-frame spectrogram JSONs     -> _run_yes
+
+Out of scope here: the spectrogram PNG (:331-348) and the blob
+uploads (``upload`` is a caller-supplied hook, default: none).
+"""
+from __future__ import annotations
+
+import os
+from typing import Callable
+
+import numpy as np
+
+from . import params as P
+from .matlab_json import encode, matlab_squeeze_2d
+
+
+# ---------------------------------------------------------------------------
+# pure host logic (testable without a GPU)
+# ---------------------------------------------------------------------------
+def measurement_update_no(per: dict, cfg: P.FmcwConfig, frame_count: int) -> dict:
+    """:157-159 + :242-252.  target_measurements.<x>(fr_idx, j) written into a
+    max_num_targets x frame_count zeros matrix grows it (MATLAB auto-expands on
+    out-of-range assignment) to max(rows) x max(cols)."""
+    M = cfg.max_targets
+    rows, cols = M, frame_count
+    entries = []
+    for f in range(frame_count):
+        n = int(per["tgt_count"][f])
+        for j in range(n):
+            entries.append((f, j, float(per["tgt_range_mag"][f, j]),
+                            float(cfg.range_m(per["tgt_range_idx"][f, j])),
+                            float(cfg.speed(per["tgt_doppler_idx"][f, j]))))
+            rows, cols = max(rows, f + 1), max(cols, j + 1)
+    out = {k: np.zeros((rows, cols)) for k in ("strength", "range", "speed")}
+    for f, j, a, r, s in entries:
+        out["strength"][f, j] = a
+        out["range"][f, j] = r
+        out["speed"][f, j] = s
+    return out
+
+
+def measurement_update_yes(per: dict, cfg: P.FmcwConfig, frames) -> dict:
+    """:499-529: (j, fr_idx) orientation, NaN where no target."""
+    M = cfg.max_targets
+    F = len(per["tgt_count"])
+    out = {k: np.zeros((M, F)) for k in ("strength", "range", "speed")}
+    for f in frames:
+        n = int(per["tgt_count"][f])
+        for j in range(M):
+            if j < n:
+                out["strength"][j, f] = per["tgt_range_mag"][f, j]
+                out["range"][j, f] = cfg.range_m(per["tgt_range_idx"][f, j])
+                out["speed"][j, f] = cfg.speed(per["tgt_doppler_idx"][f, j])
+            else:
+                for k in out:
+                    out[k][j, f] = np.nan
+    return out
+
+
+def slow_time_signal(per: dict, frames=None) -> np.ndarray:
+    """:257-260 (and :515): |X(ridx(1), :, fr)| of the frames with a target, in order."""
+    cnt = per["tgt_count"]
+    idx = np.arange(len(cnt)) if frames is None else np.asarray(list(frames))
+    keep = idx[cnt[idx] > 0]
+    return per["slow_mag"][keep].reshape(-1).astype(np.float64)
+
+
+def write_json(path: str, obj: dict) -> str:
+    with open(path, "w") as fh:
+        fh.write(encode(obj, pretty=True))
+    return path
+
+
+def write_outputs_no(out_dir: str, filename: str, cfg: P.FmcwConfig, per: dict, spec: dict,
+                     meas: dict, frame_count: int, probe_frame_index: int, probe_mag,
+                     upload: Callable[[str], None] | None = None) -> list:
+    """:302-436: the four JSON files of the 'no' branch."""
+    paths = []
+    # :306-328 spectrogram_data.json
+    paths.append(write_json(os.path.join(out_dir, "spectrogram_data.json"), {
+        "time": spec["time"], "frequency": spec["frequency"],
+        "intensity": spec["intensity"],                          # 1024 x nseg (bins down the rows)
+        "title": "All Frames - Log-Scaled Spectrogram", "xLabel": "Time (s)", "yLabel": "Frequency (Hz)"}))
+    # :355-377 <filename>_range_fft_data.json
+    time_axis = np.arange(frame_count) * 0.15
+    paths.append(write_json(os.path.join(out_dir, f"{filename}_range_fft_data.json"), {
+        "time_axis": time_axis, "array_bin_range": cfg.array_bin_range,
+        "range_tx1rx1_max_abs": matlab_squeeze_2d(per["profile"].T),   # Nr x F
+        "filename": filename}))
+    # :379-407 <filename>_range_speed_data.json
+    paths.append(write_json(os.path.join(out_dir, f"{filename}_range_speed_data.json"), {
+        "time_axis": time_axis, "range": meas["range"], "speed": meas["speed"], "filename": filename}))
+    # :409-436 <filename>_fft_data.json (linear column 100 of the Nr x PN x F cube)
+    paths.append(write_json(os.path.join(out_dir, f"{filename}_fft_data.json"), {
+        "range_bins": np.arange(cfg.nr), "magnitude": np.asarray(probe_mag, np.float64),
+        "frame_index": probe_frame_index, "filename": filename}))
+    if upload:
+        for p_ in paths:
+            upload(p_)
+    return paths
+
+
+# ---------------------------------------------------------------------------
+# the entry point (GPU)
+# ---------------------------------------------------------------------------
+def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_data: np.ndarray,
+                     device: dict, fdata: str = "radar_data", out_dir: str = ".", engine=None,
+                     upload: Callable[[str], None] | None = None, nr: int = 256, nd: int = 16,
+                     mode: str = P.PARITY) -> dict:
+    """radar_processing(process_animal_activity) with the DSP on the MI355X.
+
+    frames      [F][PN][NTS] complex: frame(fr).Chirp(:,:,1) stacked (:199-202)
+    calib_data  the calibration vector of f_parse_data2 (:86, :166-174)
+    device      sXML fields (see params.derive_params)
+    Returns the paths written and the intermediate arrays.  Raises where
+    MATLAB raises (e.g. spectrogram of fewer than 20 slow-time samples).
+    """
+    from .engine import Engine
+
+    filename = os.path.splitext(os.path.basename(fdata))[0]            # :68
+    cfg = P.derive_params(device, nr=nr, nd=nd, mode=mode)             # :89-154
+    cal = P.calibration(calib_data, cfg.n_rx, cfg.nts)                 # :166-174
+    frames = np.asarray(frames)
+    F = frames.shape[0]
+    own = engine is None
+    eng = Engine(0) if own else engine
+    try:
+        eng.set_taps(cfg, cal)                                         # :138-139 windows
+        flag = str(process_animal_activity).lower()
+        if flag == "no":
+            return _run_no(eng, cfg, frames, F, filename, out_dir, upload)
+        if flag == "yes":
+            return _run_yes(eng, cfg, frames, F, filename, out_dir, upload)
+        return {"paths": []}                                            # :195/:440: neither branch
+    finally:
+        if own:
+            eng.close()
+
+
+def _run_no(eng, cfg, frames, F, filename, out_dir, upload):
+    probe_col = 100                                                     # :410 fr_idx = 100
+    if probe_col > F * cfg.pn:
+        raise IndexError("Index exceeds the number of array elements (range_tx1rx1_complete(:,100))")
+    per = eng.process(frames, probe_column=probe_col)                   # :197-261, :265
+    meas = measurement_update_no(per, cfg, F)                           # :242-252
+    slow = slow_time_signal(per)                                        # :257-260, :270
+    fs = 1.0 / cfg.prt
+    spec = eng.stft(slow, cfg.stft_window(), cfg.overlap, fs, nfft=0, n_log_bins=1024)   # :273-299
+    spec = {"time": spec["time"].astype(np.float64), "frequency": spec["frequency"].astype(np.float64),
+            "intensity": spec["intensity"].T.astype(np.float64), "nfft": spec["nfft"]}
+    paths = write_outputs_no(out_dir, filename, cfg, per, spec, meas, F, probe_col, per["probe_mag"], upload)
+    return {"paths": paths, "per_frame": per, "target_measurements": meas, "spectrogram": spec,
+            "slow_time": slow}
+
+
+def _run_yes(eng, cfg, frames, F, filename, out_dir, upload):
+    per = eng.process(frames)                                           # :457-498 per-frame math
+    batch = cfg.batch_size                                              # :189
+    nb = -(-F // batch)                                                 # :190 ceil
+    fs = 1.0 / cfg.prt
+    paths, plot_counter, processed = [], 0, []
+    for b in range(1, nb + 1):                                          # :444
+        f0, f1 = (b - 1) * batch, min(b * batch, F)
+        processed.extend(range(f0, f1))
+        slow = slow_time_signal(per, range(f0, f1))                     # :515
+        if len(slow) == 0 or len(slow) < cfg.window_length:            # :534
+            continue
+        plot_counter += 1
+        if plot_counter > 4:                                            # :537, :598-599 break
+            break
+        spec = eng.stft(slow, cfg.stft_window(), cfg.overlap, fs, nfft=0, n_log_bins=1024)   # :538-566
+        obj = {"time": spec["time"].astype(np.float64), "frequency": spec["frequency"].astype(np.float64),
+               "intensity": spec["intensity"].T.astype(np.float64), "title": f"Spectrogram - Batch {b}",
+               "xLabel": "Time (s) (relative to detected activity)", "yLabel": "Frequency (Hz)",
+               "start_frame": f0 + 1, "end_frame": f1, "filename_base": filename}
+        p_ = write_json(os.path.join(out_dir, f"{filename}_spectrogram_batch_{b}.json"), obj)   # :587-593
+        if upload:
+            upload(p_)
+        paths.append(p_)
+    meas = measurement_update_yes(per, cfg, processed)
+    return {"paths": paths, "per_frame": per, "target_measurements": meas}

@@ -1,0 +1,100 @@
+"""GPU end to end: radar_processing('no' | 'yes') -- the drop-in entry point --
+writes the reference's JSON files with values matching the oracle pipeline."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from fmcw_radar_processing_amd import params as P
+from fmcw_radar_processing_amd import radar as R
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def calib_vector(nts, n_rx=2, dec=2):
+    cal = O.synth_cal(nts)
+    n_cal = nts * dec
+    data = np.zeros(2 * n_rx * n_cal)
+    data[0:n_cal:dec] = cal.real
+    data[n_cal:2 * n_cal:dec] = cal.imag
+    return data
+
+
+def _oracle_no(iq, nts, pn):
+    dev = P.deployed_device(nts, pn)
+    p = O.derive_params(dev, nr=256, nd=16, parity=True)
+    wr, wd = O.windows(nts, pn)
+    per = O.process_frames(iq, O.synth_cal(nts), p, wr, wd, want_cube=True)
+    meas = O.measurement_update_no(per, p, iq.shape[0])
+    x = O.slow_time_signal(per).astype(np.float32).astype(np.float64)
+    sp = O.spectrogram_pipeline(x, p["prt"], O.stft_window("kaiser"), 19)
+    return p, per, meas, sp
+
+
+def test_radar_processing_no_branch(engine, tmp_path):
+    nts, pn, F = 64, 16, 115                     # the deployed module, ~17 s of frames
+    p0 = O.derive_params(P.deployed_device(nts, pn), nr=256, nd=16)
+    iq = O.synth_frames(F, pn, nts, 256, 16, p0["dist_per_bin"])
+    res = R.radar_processing("no", frames=iq, calib_data=calib_vector(nts), device=P.deployed_device(nts, pn),
+                             out_dir=str(tmp_path), engine=engine)
+    p, per, meas, sp = _oracle_no(iq, nts, pn)
+    names = sorted(os.listdir(tmp_path))
+    assert names == sorted(["spectrogram_data.json", "radar_data_range_fft_data.json",
+                            "radar_data_range_speed_data.json", "radar_data_fft_data.json"])
+    s = json.load(open(tmp_path / "spectrogram_data.json"))
+    got = np.array(s["intensity"], dtype=np.float64)
+    assert got.shape == sp["intensity"].shape
+    sel = sp["intensity"] > -80
+    assert np.abs(got[sel] - sp["intensity"][sel]).max() < 1e-3      # fp32 dB tolerance
+    np.testing.assert_allclose(s["time"], sp["time"], rtol=1e-6)
+    np.testing.assert_allclose(s["frequency"], sp["frequency"], rtol=1e-6)
+    rs = json.load(open(tmp_path / "radar_data_range_speed_data.json"))
+    np.testing.assert_allclose(np.array(rs["range"]), meas["range"], rtol=1e-6)
+    np.testing.assert_allclose(np.array(rs["speed"]), meas["speed"], rtol=1e-6, atol=1e-9)
+    rf = json.load(open(tmp_path / "radar_data_range_fft_data.json"))
+    prof = np.array(rf["range_tx1rx1_max_abs"])
+    assert prof.shape == (256, F)
+    # fp32: per-frame relative L2 <= 1e-5 (noise-floor bins carry absolute, not relative, error)
+    err = np.linalg.norm(prof - per["profile"].T, axis=0) / np.linalg.norm(per["profile"].T, axis=0)
+    assert err.max() <= 1e-5
+    fd = json.load(open(tmp_path / "radar_data_fft_data.json"))
+    col = 99
+    want = np.abs(per["cube"][col // pn, col % pn])
+    assert np.linalg.norm(np.array(fd["magnitude"]) - want) / np.linalg.norm(want) <= 1e-5
+
+
+def test_radar_processing_yes_branch(engine, tmp_path):
+    nts, pn, F = 64, 16, 250                     # three 100-frame batches
+    p0 = O.derive_params(P.deployed_device(nts, pn), nr=256, nd=16)
+    iq = O.synth_frames(F, pn, nts, 256, 16, p0["dist_per_bin"], frame0=1000)
+    res = R.radar_processing("yes", frames=iq, calib_data=calib_vector(nts), device=P.deployed_device(nts, pn),
+                             out_dir=str(tmp_path), engine=engine)
+    assert [os.path.basename(x) for x in res["paths"]] == [f"radar_data_spectrogram_batch_{b}.json" for b in (1, 2, 3)]
+    p = O.derive_params(P.deployed_device(nts, pn), nr=256, nd=16)
+    wr, wd = O.windows(nts, pn)
+    per = O.process_frames(iq, O.synth_cal(nts), p, wr, wd)
+    for b in (1, 2, 3):
+        d = json.load(open(tmp_path / f"radar_data_spectrogram_batch_{b}.json"))
+        f0, f1 = (b - 1) * 100, min(b * 100, F)
+        keep = [f for f in range(f0, f1) if per["tgt_count"][f] > 0]
+        x = per["slow_mag"][keep].reshape(-1).astype(np.float32).astype(np.float64)
+        sp = O.spectrogram_pipeline(x, p["prt"], O.stft_window("kaiser"), 19)
+        got = np.array(d["intensity"])
+        sel = sp["intensity"] > -80
+        assert np.abs(got[sel] - sp["intensity"][sel]).max() < 1e-3
+        assert d["title"] == f"Spectrogram - Batch {b}" and d["start_frame"] == f0 + 1 and d["end_frame"] == f1
+    meas = res["target_measurements"]
+    assert meas["range"].shape == (1, F)
+    assert np.isnan(meas["range"][0, per["tgt_count"] == 0]).all()
+
+
+def test_radar_processing_no_target_raises_like_matlab(engine, tmp_path):
+    """With no detection the reference's spectrogram call errors (guard commented out at :269)."""
+    from fmcw_radar_processing_amd import FmcwError
+    nts, pn, F = 64, 16, 110
+    iq = np.tile(O.synth_cal(nts)[None, None, :], (F, pn, 1)).astype(np.complex64)   # calibration only
+    with pytest.raises(FmcwError, match="E_DATA"):
+        R.radar_processing("no", frames=iq, calib_data=calib_vector(nts), device=P.deployed_device(nts, pn),
+                           out_dir=str(tmp_path), engine=engine)

@@ -43,7 +43,8 @@ def run(cfgname, F, chunk=0, reps=5):
     e.close()
 
 if __name__ == "__main__":
-    for ch in (8, 16, 32, 64, 128, 256):
+    import sys as _s
+    chunks = [int(c) for c in _s.argv[1:]] or [64, 128, 256]
+    for ch in chunks:
         run(3, 4096, chunk=ch)
-    for ch in (32, 128):
-        run(2, 4096, chunk=ch)
+    run(2, 4096, chunk=256)
