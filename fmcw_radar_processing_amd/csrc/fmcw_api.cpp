@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -91,6 +92,9 @@ struct fmcw_ctx {
   DevBuf h_iq, h_prof, h_count, h_ridx, h_rmag, h_didx, h_slow, h_cube, h_rd, h_probe;
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
   int64_t chunk_frames = 0;
+  int pipe_mode = FMCW_PIPE_AUTO, pipe_nslot = 2;
+  DevBuf fused_ctrl, fused_slots, fused_rd_slots, fused_sticky;
+  bool fused_ran = false;
   int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
   struct Pending {
     hipEvent_t a, b;
@@ -310,6 +314,28 @@ int fmcw_set_chunk_frames(fmcw_ctx* c, int64_t frames) {
   return FMCW_OK;
 }
 
+int fmcw_set_pipeline(fmcw_ctx* c, int32_t mode, int32_t nslot) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (mode < FMCW_PIPE_AUTO || mode > FMCW_PIPE_FUSED) return fail(FMCW_E_ARG, "bad pipeline mode");
+  if (nslot != 0 && (nslot < 2 || nslot > 8)) return fail(FMCW_E_ARG, "nslot must be 0 or in [2, 8]");
+  c->pipe_mode = mode;
+  c->pipe_nslot = nslot == 0 ? 2 : nslot;
+  return FMCW_OK;
+}
+
+int fmcw_pipeline_status(fmcw_ctx* c, int32_t* status) {
+  if (!c || !status) return fail(FMCW_E_ARG, "NULL argument");
+  CHK(set_device(c));
+  *status = 0;
+  if (!c->fused_sticky.p) return FMCW_OK;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned v = 0;
+  HIPCHK(hipMemcpy(&v, c->fused_sticky.p, 4, hipMemcpyDeviceToHost));
+  if (v) HIPCHK(hipMemset(c->fused_sticky.p, 0, 4));
+  *status = (int32_t)v;
+  return FMCW_OK;
+}
+
 int fmcw_synchronize(fmcw_ctx* c) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   CHK(set_device(c));
@@ -359,6 +385,57 @@ int fmcw_timing_reset(fmcw_ctx* c) {
 // ---------------------------------------------------------------------------
 // per-frame stages
 // ---------------------------------------------------------------------------
+// One persistent launch (kernels_fused.hip): the range cube of each frame
+// lives in a per-XCD slot instead of HBM.  d_rd == nullptr keeps the RD maps
+// in per-XCD slots too (detect is their only consumer).
+static int process_fused(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
+                         float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
+                         float* d_slow, void* d_rd, int32_t rd_dt, int64_t probe_column, float* d_probe,
+                         hipStream_t s) {
+  const int C = p->pn, NR = p->nr, ND = p->nd, ns = c->pipe_nslot;
+  const size_t words = (size_t)fmcw::fused_ctrl_words(F);
+  CHK(c->fused_ctrl.ensure(words * 4));
+  CHK(c->fused_slots.ensure((size_t)8 * ns * C * NR * 8));
+  if (!d_rd) CHK(c->fused_rd_slots.ensure((size_t)8 * ns * NR * ND * esize(rd_dt)));
+  if (!c->fused_sticky.p) {
+    CHK(c->fused_sticky.ensure(4));
+    HIPCHK(hipMemsetAsync(c->fused_sticky.p, 0, 4, s));
+  }
+  HIPCHK(hipMemsetAsync(c->fused_ctrl.p, 0, words * 4, s));
+  fmcw::FusedArgs a{};
+  a.iq = d_iq; a.in_dtype = in_dtype; a.F = F;
+  a.C = C; a.S = p->nts; a.NR = NR; a.ND = ND;
+  a.calw = c->calw.as<float4>(); a.cal_sum = c->cal_sum; a.if_scale = p->if_scale;
+  a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
+  a.rd = d_rd; a.rd_dtype = rd_dt;
+  a.rd_scale = rd_dt == FMCW_C32H ? 1.0f / ((float)NR * ND) : 1.0f;
+  a.rd_slots = d_rd ? nullptr : c->fused_rd_slots.p;
+  a.profile = d_prof;
+  a.slots = c->fused_slots.as<float2>();
+  a.nslot = ns;
+  a.ctrl = c->fused_ctrl.as<unsigned>();
+  a.spin_limit = 1u << 22;           // ~ seconds of polling: only a broken schedule gets there
+  a.sticky = c->fused_sticky.as<unsigned>();
+  {
+    const char* e = std::getenv("FMCW_FUSED_STRICT");
+    a.strict = (e && e[0] == '1') ? 1 : 0;
+  }
+  a.det.ND = ND; a.det.C = C; a.det.M = p->max_targets;
+  a.det.range_thr = p->range_thr; a.det.doppler_thr = p->doppler_thr;
+  a.det.min_d = p->min_d; a.det.max_d = p->max_d; a.det.dist_per_bin = p->dist_per_bin;
+  a.det.fallback = p->doppler_fallback_idx;
+  a.det.cube_unscale = 1.0f; a.det.rd_unscale = 1.0f / a.rd_scale;
+  a.count = d_count; a.ridx = d_ridx; a.rmag = d_rmag; a.didx = d_didx; a.slow_mag = d_slow;
+  a.probe_frame = probe_column > 0 ? (probe_column - 1) / C : -1;
+  a.probe_chirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
+  a.probe_mag = d_probe;
+  StageTimer span(c, 7, s, 1);
+  HIPCHK(fmcw::launch_fused(a, s));
+  span.done();
+  c->fused_ran = true;
+  return FMCW_OK;
+}
+
 int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
                         float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
                         float* d_slow, void* d_cube, void* d_rd, int32_t out_dtype, int64_t probe_column,
@@ -373,6 +450,12 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
   if (probe_column < 0 || probe_column > F * (int64_t)C) return fail(FMCW_E_ARG, "probe_column out of range");
   hipStream_t s = pick(c, stream);
+  const bool fusable = !d_cube && fmcw::fused_supported(NR, ND);
+  if (c->pipe_mode == FMCW_PIPE_FUSED && !fusable)
+    return fail(FMCW_E_ARG, "fused schedule: no fused kernel for this geometry, or a range cube was requested");
+  if (fusable && c->pipe_mode != FMCW_PIPE_STREAMS)
+    return process_fused(c, p, d_iq, in_dtype, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd,
+                         d_rd ? out_dtype : FMCW_C64, probe_column, d_probe, s);
   const int64_t chunk = c->chunk_frames > 0 ? c->chunk_frames : default_chunk(p);
   const int cube_dt = d_cube ? out_dtype : FMCW_C64;
   const int rd_dt = d_rd ? out_dtype : FMCW_C64;
@@ -711,6 +794,11 @@ int fmcw_process(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_d
   if (rd) HIPCHK(hipMemcpyAsync(rd, c->h_rd.p, (size_t)F * NR * ND * 8, hipMemcpyDeviceToHost, s));
   if (probe) HIPCHK(hipMemcpyAsync(probe, c->h_probe.p, (size_t)NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (c->fused_ran) {
+    int32_t st = 0;
+    CHK(fmcw_pipeline_status(c, &st));
+    if (st) return fail(FMCW_E_HIP, "fused schedule: a bounded wait timed out; results are invalid");
+  }
   return FMCW_OK;
 }
 

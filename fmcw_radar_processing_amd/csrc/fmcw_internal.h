@@ -54,6 +54,50 @@ struct DetectArgs {
   float* probe_mag;        // [NR]
 };
 
+// detection constants shared by k_detect and the fused kernel (frame_ops.h)
+struct DetectParams {
+  int ND, C, M;
+  float range_thr, doppler_thr, min_d, max_d, dist_per_bin;
+  int fallback;
+  float cube_unscale, rd_unscale;
+};
+
+// persistent XCD-local range+Doppler+detect (kernels_fused.hip)
+struct FusedArgs {
+  const void* iq;          // [F][C][S]
+  int in_dtype;
+  int64_t F;
+  int C, S, NR, ND;
+  const float4* calw;
+  float2 cal_sum;
+  float if_scale;
+  const float2* tw_nr;     // [NR]
+  const float2* tw_nd;     // [ND]
+  const float* wd;         // [C]
+  void* rd;                // [F][NR][ND], or nullptr: RD lives in per-XCD slots (rd_slots)
+  int rd_dtype;
+  float rd_scale;
+  void* rd_slots;          // [8][nslot][NR][ND] of rd_dtype when rd == nullptr
+  float* profile;          // [F][NR]
+  float2* slots;           // [8 XCDs][nslot][C][NR] fp32 cube slots
+  int nslot;               // >= 2
+  unsigned* ctrl;          // zeroed per launch: 8 heads (128 B apart), k1done[F], k2done[F], done[F], err
+  unsigned spin_limit;
+  unsigned* sticky;        // set to 1 on a spin timeout; cleared only by fmcw_pipeline_status
+  int strict;              // 1: agent release/acquire at every hand-off (placement-independent form)
+  DetectParams det;
+  int32_t* count;
+  int32_t* ridx;
+  float* rmag;
+  int32_t* didx;
+  float* slow_mag;
+  int64_t probe_frame;     // global frame, -1 = none
+  int probe_chirp;
+  float* probe_mag;
+};
+
+inline int64_t fused_ctrl_words(int64_t F) { return 256 + 3 * F + 1; }
+
 struct StftArgs {
   const float* slow_mag;   // [*][pn]
   const int32_t* frame_list;
@@ -101,6 +145,9 @@ hipError_t launch_stft_power(const StftArgs& a, hipStream_t s);
 hipError_t launch_stft_db(const StftDbArgs& a, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s);
+
+hipError_t launch_fused(const FusedArgs& a, hipStream_t s);
+bool fused_supported(int nr, int nd);
 
 bool range_size_supported(int nr);
 bool doppler_size_supported(int nd);

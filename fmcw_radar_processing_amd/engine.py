@@ -76,6 +76,16 @@ class Engine:
     def set_chunk_frames(self, n: int) -> None:
         check(self.lib.fmcw_set_chunk_frames(self.h, int(n)))
 
+    def set_pipeline(self, mode: int, nslot: int = 0) -> None:
+        """FMCW_PIPE_AUTO / _STREAMS / _FUSED (include/fmcw.h); nslot cube slots per XCD."""
+        check(self.lib.fmcw_set_pipeline(self.h, int(mode), int(nslot)))
+
+    def pipeline_status(self) -> int:
+        """0, or 1 when a fused launch since the last query hit a bounded-wait timeout."""
+        st = ct.c_int32(0)
+        check(self.lib.fmcw_pipeline_status(self.h, ct.byref(st)))
+        return st.value
+
     # ---- host-array API --------------------------------------------------------
     def process(self, iq: np.ndarray, want_cube: bool = False, want_rd: bool = False,
                 probe_column: int = 0) -> dict:

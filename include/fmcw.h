@@ -209,10 +209,29 @@ int fmcw_timing_enable(fmcw_ctx* ctx, int32_t enable);
 int fmcw_timing_read(fmcw_ctx* ctx, int32_t stage, double* total_ms, int64_t* launches);
 int fmcw_timing_reset(fmcw_ctx* ctx);
 
-/* Frames per range/Doppler chunk (the range cube of one chunk is the only
- * intermediate; it is sized to stay in the 256 MiB Infinity Cache).
+/* Frames per range/Doppler chunk of the 3-stream pipeline (the range cube of
+ * one chunk is its only intermediate; default 256 MiB of cube per chunk).
  * 0 restores the default. */
 int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
+
+/* Schedule of fmcw_process_device / fmcw_process (results are identical):
+ *  FMCW_PIPE_AUTO    fused when the geometry has a fused kernel and no range
+ *                    cube is requested, otherwise streams (default);
+ *  FMCW_PIPE_STREAMS K1 | K2 | K3 kernels as a 3-stream chunk pipeline, the
+ *                    range cube of each chunk round-trips through HBM;
+ *  FMCW_PIPE_FUSED   one persistent kernel per call: each XCD runs its frames'
+ *                    range, Doppler and detect items from a ticket queue, the
+ *                    range cube of a frame stays in that XCD's L2.  E_ARG when
+ *                    the geometry has no fused kernel or a cube is requested.
+ * nslot (>= 2, 0 = default 2): cube slots per XCD for the fused schedule. */
+enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_FUSED = 2 };
+int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode, int32_t nslot);
+
+/* Fused-schedule health after the last call (synchronises the stream):
+ * 0 = every wait was satisfied, 1 = a bounded spin timed out (results of
+ * that call are invalid; the call itself also returned FMCW_E_HIP when it
+ * synchronised). */
+int fmcw_pipeline_status(fmcw_ctx* ctx, int32_t* status);
 
 int fmcw_synchronize(fmcw_ctx* ctx);
 

@@ -1,0 +1,14 @@
+#!/bin/bash
+# rocprofv3 passes over tools/perf_probe.py: kernel stats, then one PMC group per pass.
+# usage: tools/profile_probe.sh <tag> <probe args...>
+set -o pipefail
+tag=$1; shift
+out=gpurun_out/pp_$tag
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/stats -o run --output-format csv -- python3 tools/perf_probe.py "$@" > $out/stats.log 2>&1 || exit 11
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $out/fetch -o run --output-format csv -- python3 tools/perf_probe.py "$@" > $out/fetch.log 2>&1 || exit 12
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $out/write -o run --output-format csv -- python3 tools/perf_probe.py "$@" > $out/write.log 2>&1 || exit 13
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_LDS_BANK_CONFLICT --kernel-trace -d $out/sq -o run --output-format csv -- python3 tools/perf_probe.py "$@" > $out/sq.log 2>&1 || exit 14
+timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --kernel-trace -d $out/tcc -o run --output-format csv -- python3 tools/perf_probe.py "$@" > $out/tcc.log 2>&1 || exit 15
+echo done
