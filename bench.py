@@ -127,7 +127,9 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    level = 0 if args.no_stage_timing else 1
+    # level 2: HIP events around every K1/K2/K3 launch on its own stream (the
+    # per-kernel roofline below) plus the range+Doppler span and STFT launches
+    level = 0 if args.no_stage_timing else 2
     eng.timing(level)
     eng.timing_reset()
     barrier()
@@ -150,21 +152,53 @@ def main():
     # sanity: the step did real work (detections on most frames)
     det = int((outs["tgt_count"] > 0).sum().item())
 
-    # ---- roofline of the range+Doppler chunk (K1 range FFT + K2 Doppler FFT) --------
+    # ---- roofline ----------------------------------------------------------------
+    # path: SURVEY.md 8d config-4 algorithmic bytes per frame (input + RD map +
+    # profile + slow-time row; the range cube is an intermediate) over the
+    # range+Doppler span.  dominant kernel: k_range (K1), whose own algorithmic
+    # bytes are its input and the range cube it materialises (the config-2
+    # per-frame figure without the profile), over its HIP-event launch time.
     esz = 4 if args.fp16 else 8
-    alg_per_frame = C * S * esz + NR * ND * esz + NR * 4 + C * 4    # in + RD + profile + slow row
-    roof = None
+    alg_per_frame = C * S * esz + NR * ND * esz + NR * 4 + C * 4
+    k1_per_frame = C * S * esz + C * NR * 8          # streams schedule keeps an fp32 cube
+    kern = {}
+    for name, label, per_frame in (("range", "k_range", k1_per_frame), ("doppler", "k_doppler", C * NR * 8 + NR * ND * esz + NR * 4),
+                                   ("detect", "k_detect", None)):
+        ms, n = stages.get(name, (0.0, 0))
+        if n:
+            fpl = F * args.steps / n
+            us = ms / n * 1e3
+            kern[label] = {"avg_launch_us": round(us, 2), "frames_per_launch": fpl}
+            if per_frame:
+                kern[label]["alg_bytes_per_launch"] = int(per_frame * fpl)
+                kern[label]["achieved_GBps"] = round(per_frame * fpl / (us * 1e-6) / 1e9, 1)
+    roof, path = None, None
     rd_ms, rd_n = stages.get("range_doppler", (0.0, 0))
     if rd_n:
         per_launch_ms = rd_ms / rd_n
-        frames_per_launch = F * args.steps / rd_n
-        achieved = alg_per_frame * frames_per_launch / (per_launch_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                "kernel": "range+Doppler span: k_range || k_doppler chunk pipeline over 3 HIP streams "
-                          "(HIP events: before first k_range .. after last k_doppler)",
-                "avg_launch_us": round(per_launch_ms * 1e3, 2), "frames_per_launch": frames_per_launch,
-                "alg_bytes_per_frame": alg_per_frame}
+        fpl = F * args.steps / rd_n
+        ach = alg_per_frame * fpl / (per_launch_ms * 1e-3) / 1e9
+        path = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4), "unit": "GB/s",
+                "span_us": round(per_launch_ms * 1e3, 2), "frames_per_span": fpl, "alg_bytes_per_frame": alg_per_frame,
+                "what": "range+Doppler span (before first k_range .. after last k_doppler), SURVEY 8d bytes"}
+    pmc = load_pmc(os.path.join(ROOT, "profiles"), args)
+    if "k_range" in kern:
+        k = kern["k_range"]
+        traffic = None
+        if pmc and "k_range" in pmc.get("kernels", {}):
+            pk = pmc["kernels"]["k_range"]
+            if abs(pk.get("frames_per_launch", 0) - k["frames_per_launch"]) < 0.5:
+                traffic = pk.get("hbm_bytes_per_launch")
+        roof = {"bound": "hbm", "achieved": k["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(k["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": "k_range (K1: calibration, mean removal, window, 1024-pt range FFT, cube store)",
+                "alg_bytes_per_launch": k["alg_bytes_per_launch"], "avg_launch_us": k["avg_launch_us"],
+                "frames_per_launch": k["frames_per_launch"],
+                "traffic_source": pmc.get("source") if pmc and traffic else None}
+    elif path:
+        roof = {"bound": "hbm", "achieved": path["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": path["frac"], "traffic": None, "kernel": "k_rd_fused (one launch per step)",
+                "avg_launch_us": path["span_us"], "frames_per_launch": path["frames_per_span"]}
 
     # ---- input fan-out over xGMI from rank 0 (reported separately, not in value) -----
     fanout = None
@@ -186,7 +220,7 @@ def main():
         del src, dst
 
     if rank == 0:
-        cpu = cpu_baseline(args.cpu_seconds) if args.cpu_seconds > 0 else None
+        cpu = cpu_baseline(args.cpu_seconds, d_iq, F, dt) if args.cpu_seconds > 0 else None
         total_frames = world * F * args.steps
         value = total_frames / elapsed
         line = {
@@ -202,6 +236,8 @@ def main():
                        "parallelism": f"frame-shard dp{world}"},
             "hbm_alg_GBps": round(alg_per_frame * value / world / 1e9, 1),
             "roofline": roof,
+            "path_roofline": path,
+            "kernels": kern,
             "cpu_baseline": cpu,
             "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items() if v[1]},
             "frames_with_target": det,
@@ -213,33 +249,70 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(budget_s: float):
-    """Oracle (fp64 numpy restatement of radar_processing.m:197-299) on a bounded
-    sample of the same config-4 workload, on this host, 1 thread."""
-    os.environ.setdefault("OMP_NUM_THREADS", "1")
+def load_pmc(pdir: str, args):
+    """Per-launch HBM traffic of the dominant kernel from the committed rocprofv3
+    PMC summary of this same command (tools/profile_run.sh -> profiles/*pmc*.json):
+    FETCH_SIZE x 2 (gfx950 read correction, MI355X_MICROARCH.md HBM section) +
+    WRITE_SIZE, averaged over the kernel's dispatches."""
+    name = "bench_fp16_pmc.json" if args.fp16 else "bench_pmc.json"
+    path = os.path.join(pdir, name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    d["source"] = os.path.relpath(path, ROOT)
+    return d
+
+
+def cpu_baseline(budget_s: float, d_iq, F: int, dt: int):
+    """C restatement of radar_processing.m:197-299 (oracle/fmcw_oracle.c, fp64,
+    OpenMP over frames) on a bounded sample of the SAME device-resident frames
+    (copied back in batches), on this host's cores.  Every row's Doppler FFT is
+    computed (as the GPU path does), then the hop-1 STFT of the slow-time signal."""
+    import torch
     from fmcw_radar_processing_amd import params as P
+    from oracle import coracle as CO
     from oracle import oracle as O
+    try:
+        cores = min(16, len(os.sched_getaffinity(0)))
+    except AttributeError:
+        cores = min(16, os.cpu_count() or 1)
     cfg = P.config(4)
     p = O.derive_params(P.deployed_device(cfg.nts, cfg.pn), nr=cfg.nr, nd=cfg.nd, parity=False)
     wr, wd = O.windows(cfg.nts, cfg.pn)
-    cal = O.synth_cal(cfg.nts)
+    cal = P.synth_calibration(cfg.nts)
     win = O.stft_window("hann")
-    done, slow, busy = 0, [], 0.0
-    while busy < budget_s or done < 8:
-        iq = O.synth_frames(4, cfg.pn, cfg.nts, cfg.nr, cfg.nd, p["dist_per_bin"], frame0=done)  # not timed
+    B = 4 * cores
+
+    def batch(f0):
+        x = d_iq[f0:f0 + B].float().cpu().numpy()            # fp16 storage: the same values widened
+        return x.view(np.float32).reshape(x.shape[0], cfg.pn, cfg.nts, 2).view(np.complex64)[..., 0]
+
+    def run(threads, budget):
+        done, slow, busy = 0, [], 0.0
+        rd = np.zeros((B, cfg.nr, cfg.nd), np.complex128)
+        f0 = 0
+        while busy < budget or done < B:
+            iq = batch(f0)                                      # not timed
+            t = time.perf_counter()
+            out = CO.process_frames(iq, cal, p, wr, wd, rd_out=rd[:iq.shape[0]], nthreads=threads)
+            keep = out["tgt_count"] > 0
+            slow.append(out["slow_mag"][keep].reshape(-1))
+            busy += time.perf_counter() - t
+            done += iq.shape[0]
+            f0 = (f0 + B) % max(F - B, 1)
         t = time.perf_counter()
-        out = O.process_frames(iq, cal, p, wr, wd, rd_all_rows=True)
-        slow.append(O.slow_time_signal(out))
-        busy += time.perf_counter() - t
-        done += 4
-    t = time.perf_counter()
-    x = np.concatenate(slow)
-    if len(x) >= STFT_WLEN:
-        O.spectrogram_pipeline(x, cfg.prt, win, STFT_NOVERLAP, nfft=STFT_NFFT, nbins=0)
-    elapsed = busy + time.perf_counter() - t
-    return {"value": round(done / elapsed, 2), "unit": "frames/s", "cores": 1, "kind": "port",
-            "sample": f"{done} frames of the config-4 workload through oracle/oracle.py "
-                      "(fp64 numpy restatement, 1 thread)"}
+        x = np.concatenate(slow)
+        if len(x) >= STFT_WLEN:
+            CO.spectrogram(x, cfg.prt, win, STFT_NOVERLAP, STFT_NFFT, nbins=0, nthreads=threads)
+        return done / (busy + time.perf_counter() - t), done
+
+    v_all, n_all = run(cores, budget_s)
+    v_one, n_one = run(1, max(2.0, budget_s / 4))
+    return {"value": round(v_all, 2), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{n_all} config-4 frames (the bench's own device frames, copied back) through "
+                      f"oracle/fmcw_oracle.c (fp64, OpenMP {cores} threads, every RD row) + hop-1 STFT nfft 64",
+            "single_thread": {"value": round(v_one, 2), "frames": n_one}}
 
 
 if __name__ == "__main__":

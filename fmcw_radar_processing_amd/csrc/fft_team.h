@@ -153,40 +153,106 @@ template <int N> struct FftPlan {
 
 __device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
 
-// Twiddle w^r (r = 1..R-1) for a pass, with w = tw[k * stride].  Only w^1, w^2,
-// w^4, w^8 come from the table; the others are formed with at most two
-// complex products (fewer loads in flight, fewer VGPRs, error <= ~3 ulp).
-template <int R>
-__device__ __forceinline__ void pass_twiddles(float2* w, const float2* __restrict__ tw, int base, int mask) {
-  w[1] = tw[base & mask];
-  if constexpr (R > 2) w[2] = tw[(2 * base) & mask];
-  if constexpr (R > 2) w[3] = cmul(w[1], w[2]);
-  if constexpr (R > 4) {
-    w[4] = tw[(4 * base) & mask];
-    w[5] = cmul(w[4], w[1]); w[6] = cmul(w[4], w[2]); w[7] = cmul(w[4], w[3]);
+constexpr int fft_num_r16(int n) { return n >= 16 ? 1 + fft_num_r16(n / 16) : 0; }
+constexpr int fft_pow16(int k) { return k == 0 ? 1 : 16 * fft_pow16(k - 1); }
+constexpr int tw_nb(int R) { return R >= 16 ? 4 : R >= 8 ? 3 : R >= 4 ? 2 : R >= 2 ? 1 : 0; }
+
+// Pass structure of an N-point transform: radix-16 passes, then radix R0.
+template <int N> struct FftPasses {
+  static constexpr int NR16 = fft_num_r16(N);
+  static constexpr int R0 = N / fft_pow16(NR16);
+  static constexpr int NPASS = NR16 + (R0 > 1 ? 1 : 0);
+  static constexpr int radix(int p) { return p < NR16 ? 16 : R0; }
+  static constexpr int q(int p) { return FftPlan<N>::P / radix(p); }
+  // offset of pass p's base twiddles in a preloaded block (pass 0 has none)
+  static constexpr int off(int p) {
+    int o = 0;
+    for (int i = 1; i < p; ++i) o += q(i) * tw_nb(radix(i));
+    return o;
   }
-  if constexpr (R > 8) {
-    w[8] = tw[(8 * base) & mask];
+  static constexpr int NB = off(NPASS) > 0 ? off(NPASS) : 1;
+};
+
+// Twiddle sources for a pass.  TwTable reads w^1, w^2, w^4, w^8 from the
+// table where the pass needs them; TwPre takes them from a block a kernel
+// loaded up front (load_tw_bases), so a kernel that prefetches the next
+// chirp never waits on a twiddle load queued behind it (vmcnt is in order).
+// Both give bit-identical twiddles.
+struct TwTable {
+  const float2* __restrict__ tw;
+  // b[0..nb-1] = w^1, w^2, w^4, w^8 with w = tw[k * N/(Ns*R)]
+  template <int N, int PASS, int R, int Ns>
+  __device__ __forceinline__ void get(float2* b, int q, int t) const {
+    constexpr int T = FftPlan<N>::T, nb = tw_nb(R);
+    const int k = (t + T * q) & (Ns - 1);
+    const int base = k * (N / (Ns * R));
+    b[0] = tw[base & (N - 1)];
+    if constexpr (nb > 1) b[1] = tw[(2 * base) & (N - 1)];
+    if constexpr (nb > 2) b[2] = tw[(4 * base) & (N - 1)];
+    if constexpr (nb > 3) b[3] = tw[(8 * base) & (N - 1)];
+  }
+};
+
+struct TwPre {
+  const float2* tb;      // FftPasses<N>::NB values from load_tw_bases<N>
+  template <int N, int PASS, int R, int Ns>
+  __device__ __forceinline__ void get(float2* b, int q, int) const {
+    constexpr int nb = tw_nb(R), o = FftPasses<N>::off(PASS);
 #pragma unroll
-    for (int r = 9; r < 16; ++r) w[r] = cmul(w[8], w[r - 8]);
+    for (int i = 0; i < nb; ++i) b[i] = tb[o + q * nb + i];
+  }
+};
+
+// v[r] *= w^r for r = 1..R-1, from the bases w^1, w^2, w^4, w^8: one complex
+// product per set bit of r (<= 4 roundings, like a product-formed table, but
+// only the four bases stay live -- the FFT passes are register-bound).
+template <int R>
+__device__ __forceinline__ void apply_twiddles(float2* v, const float2* b) {
+#pragma unroll
+  for (int r = 1; r < R; ++r) {
+    float2 x = v[r];
+    if (r & 1) x = cmul(x, b[0]);
+    if (r & 2) x = cmul(x, b[1]);
+    if (r & 4) x = cmul(x, b[2]);
+    if (r & 8) x = cmul(x, b[3]);
+    v[r] = x;
+  }
+}
+
+template <int N, int PASS = 1>
+__device__ __forceinline__ void load_tw_bases(float2* tb, int t, const float2* __restrict__ tw) {
+  using F = FftPasses<N>;
+  if constexpr (PASS < F::NPASS) {
+    constexpr int R = F::radix(PASS), Q = F::q(PASS), nb = tw_nb(R), o = F::off(PASS);
+    constexpr int T = FftPlan<N>::T;
+    int Ns = 1;
+#pragma unroll
+    for (int i = 0; i < PASS; ++i) Ns *= F::radix(i);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int k = (t + T * q) & (Ns - 1);
+      const int base = k * (N / (Ns * R));
+      tb[o + q * nb] = tw[base & (N - 1)];
+      if constexpr (nb > 1) tb[o + q * nb + 1] = tw[(2 * base) & (N - 1)];
+      if constexpr (nb > 2) tb[o + q * nb + 2] = tw[(4 * base) & (N - 1)];
+      if constexpr (nb > 3) tb[o + q * nb + 3] = tw[(8 * base) & (N - 1)];
+    }
+    load_tw_bases<N, PASS + 1>(tb, t, tw);
   }
 }
 
 // One Stockham pass of radix R with stride Ns on registers in butterfly layout
 // v[q*R + r] = in[t + T*q + r*N/R].  Applies the inter-pass twiddles and the
 // radix-R DFTs in place.
-template <int N, int R, int Ns>
-__device__ __forceinline__ void stockham_pass_regs(float2* v, int t, const float2* __restrict__ tw) {
-  constexpr int P = FftPlan<N>::P, T = FftPlan<N>::T, Q = P / R;
+template <int N, int PASS, int R, int Ns, class TW>
+__device__ __forceinline__ void stockham_pass_regs(float2* v, int t, const TW& src) {
+  constexpr int P = FftPlan<N>::P, Q = P / R;
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
     if constexpr (Ns > 1) {
-      const int j = t + T * q;
-      const int k = j & (Ns - 1);
-      float2 w[R];
-      pass_twiddles<R>(w, tw, k * (N / (Ns * R)), N - 1);
-#pragma unroll
-      for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], w[r]);
+      float2 b[4];
+      src.template get<N, PASS, R, Ns>(b, q, t);
+      apply_twiddles<R>(v + q * R, b);
     }
     dft<R>(v + q * R);
   }
@@ -215,26 +281,21 @@ __device__ __forceinline__ void stockham_load_lds(float2* v, int t, const float2
     for (int r = 0; r < R; ++r) v[q * R + r] = lds[lds_pad(t + T * q + r * (N / R))];
 }
 
-constexpr int fft_num_r16(int n) { return n >= 16 ? 1 + fft_num_r16(n / 16) : 0; }
-constexpr int fft_pow16(int k) { return k == 0 ? 1 : 16 * fft_pow16(k - 1); }
-
 // Recursive pass driver.  `PASS` indexes the pass, Ns = product of radices so far.
-template <int N, int PASS, int Ns, class Sync>
-__device__ __forceinline__ void team_fft_passes(float2* v, float2* lds, int t, const float2* __restrict__ tw,
-                                                Sync sync) {
-  constexpr int NR16 = fft_num_r16(N);
-  constexpr int R0 = N / fft_pow16(NR16);           // remainder radix (1, 2, 4, 8)
-  constexpr int NPASS = NR16 + (R0 > 1 ? 1 : 0);
+template <int N, int PASS, int Ns, class Sync, class TW>
+__device__ __forceinline__ void team_fft_passes(float2* v, float2* lds, int t, const TW& src, Sync sync) {
+  using F = FftPasses<N>;
+  constexpr int NR16 = F::NR16, R0 = F::R0, NPASS = F::NPASS;
   constexpr int R = (PASS < NR16) ? 16 : R0;
   constexpr int P = FftPlan<N>::P, Q = P / R;
-  stockham_pass_regs<N, R, Ns>(v, t, tw);
+  stockham_pass_regs<N, PASS, R, Ns>(v, t, src);
   if constexpr (PASS + 1 < NPASS) {
     constexpr int RN = (PASS + 1 < NR16) ? 16 : R0;
     sync();                      // previous readers of `lds` are done (WAR)
     stockham_store_lds<N, R, Ns>(v, t, lds);
     sync();                      // stores visible (RAW)
     stockham_load_lds<N, RN>(v, t, lds);
-    team_fft_passes<N, PASS + 1, Ns * R, Sync>(v, lds, t, tw, sync);
+    team_fft_passes<N, PASS + 1, Ns * R, Sync>(v, lds, t, src, sync);
   } else {
     // last pass: the butterfly layout v[q*R + r] holds X[t + T*(q + r*Q)];
     // permute to the cyclic layout v[m] = X[t + T*m] (compile-time moves).
@@ -255,7 +316,12 @@ __device__ __forceinline__ void team_fft_passes(float2* v, float2* lds, int t, c
 // `sync` must order LDS accesses of all threads of the team.
 template <int N, class Sync>
 __device__ __forceinline__ void team_fft(float2* v, float2* lds, int t, const float2* __restrict__ tw, Sync sync) {
-  team_fft_passes<N, 0, 1, Sync>(v, lds, t, tw, sync);
+  team_fft_passes<N, 0, 1, Sync>(v, lds, t, TwTable{tw}, sync);
+}
+// Same transform with the base twiddles preloaded by load_tw_bases<N>.
+template <int N, class Sync>
+__device__ __forceinline__ void team_fft_pre(float2* v, float2* lds, int t, const float2* tb, Sync sync) {
+  team_fft_passes<N, 0, 1, Sync>(v, lds, t, TwPre{tb}, sync);
 }
 
 struct BlockSync {

@@ -225,6 +225,15 @@ int64_t default_chunk(const fmcw_params* p) {
   return std::max<int64_t>(c, 1);
 }
 
+// Chirps per K1 team: long enough streams for the next-chirp prefetch, while
+// keeping >= ~2048 workgroups per launch to fill 256 CUs.
+int range_cpt(int nr, int64_t nchirps) {
+  const int T = nr >= 16 ? nr / 16 : 1;
+  const int teams = T >= 256 ? 1 : 256 / T;
+  const int64_t c = nchirps / ((int64_t)teams * 2048);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(8, c));
+}
+
 hipStream_t pick(fmcw_ctx* c, void* stream) { return stream ? static_cast<hipStream_t>(stream) : c->stream; }
 
 }  // namespace
@@ -453,7 +462,10 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const bool fusable = !d_cube && fmcw::fused_supported(NR, ND);
   if (c->pipe_mode == FMCW_PIPE_FUSED && !fusable)
     return fail(FMCW_E_ARG, "fused schedule: no fused kernel for this geometry, or a range cube was requested");
-  if (fusable && c->pipe_mode != FMCW_PIPE_STREAMS)
+  // AUTO = streams: with a 2 MiB fp32 range cube per frame two frames in
+  // flight do not fit one XCD's 4 MiB L2, so the fused schedule moves the same
+  // HBM bytes as the streams one and is slower (fused schedule)
+  if (fusable && c->pipe_mode == FMCW_PIPE_FUSED)
     return process_fused(c, p, d_iq, in_dtype, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd,
                          d_rd ? out_dtype : FMCW_C64, probe_column, d_probe, s);
   const int64_t chunk = c->chunk_frames > 0 ? c->chunk_frames : default_chunk(p);
@@ -473,6 +485,7 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
   const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
   hipStream_t sd = c->sd, sx = c->sx;
+  if (const char* e = std::getenv("FMCW_ONE_STREAM"); e && e[0] == '1') sd = sx = s;   // A/B probe
   StageTimer span(c, 7, s, 1);     // range+Doppler span: before K1(0) on s ... after the last K2 on sd
   HIPCHK(hipEventRecord(c->ev_fork, s));
   HIPCHK(hipStreamWaitEvent(sd, c->ev_fork, 0));
@@ -501,7 +514,7 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
     ra.cube_dtype = cube_dt;
     ra.cube_scale = cube_scale;
     ra.profile = nullptr;
-    ra.cpt = 1;
+    ra.cpt = range_cpt(NR, ra.nchirps);
     {
       StageTimer tm(c, 0, s, 2);
       HIPCHK(fmcw::launch_range(ra, s));

@@ -156,6 +156,67 @@ __device__ __forceinline__ void range_team(const TIn* __restrict__ x, bool valid
 }
 
 // ---------------------------------------------------------------------------
+// Streaming form of range_team for K1 (k_range): the caller keeps the next
+// chirp's loads in flight while this chirp is transformed.
+//   chirp_load    issues the P sample loads of one chirp (branch-free)
+//   chirp_finish  mean removal, calibration (taps from LDS), window, FFT with
+//                 preloaded twiddles, store.  Same arithmetic, in the same
+//                 order, as range_team.
+// ---------------------------------------------------------------------------
+template <int NR, typename TIn>
+__device__ __forceinline__ void chirp_load(const TIn* __restrict__ x, bool valid, int nmax, int t,
+                                           float2 (&v)[FftPlan<NR>::P]) {
+  using Plan = FftPlan<NR>;
+  if (nmax == NR) {
+    // whole chirp in range (S >= Nr): one base address + immediate offsets.
+    // x is a readable chirp even when !valid; chirp_finish zeroes those.
+    const TIn* __restrict__ xb = x + t;
+#pragma unroll
+    for (int m = 0; m < Plan::P; ++m) v[m] = ld_c(xb, Plan::T * m);
+  } else {
+#pragma unroll
+    for (int m = 0; m < Plan::P; ++m) {
+      const int n = t + Plan::T * m;
+      v[m] = ld_c(x, (valid && n < nmax) ? n : 0);
+    }
+  }
+}
+
+template <int NR, typename TIn, typename TCube>
+__device__ __forceinline__ void chirp_finish(float2 (&v)[FftPlan<NR>::P], const TIn* __restrict__ x, bool valid,
+                                             TCube* __restrict__ o, int S, const float4* taps, float2 cal_sum,
+                                             float cube_scale, const float2* tb, float2* my, float2* myred, int t) {
+  using Plan = FftPlan<NR>;
+  constexpr int P = Plan::P, T = Plan::T;
+  using Sync = typename TeamSync<T>::type;
+  const int nmax = S < NR ? S : NR;
+  float2 s = make_float2(0.f, 0.f);
+#pragma unroll
+  for (int m = 0; m < P; ++m) {
+    const int n = t + T * m;
+    if (!(valid && n < nmax)) v[m] = make_float2(0.f, 0.f);
+    s = cadd(s, v[m]);
+  }
+  if (S > NR && valid) {
+    for (int n = NR + t; n < S; n += T) s = cadd(s, ld_c(x, n));
+  }
+  s = team_sum<T>(s, myred, t);
+  const float2 mu = cscale(csub(s, cal_sum), 1.0f / (float)S);
+#pragma unroll
+  for (int m = 0; m < P; ++m) {
+    const int n = t + T * m;
+    const float4 c = taps[n < nmax ? n : 0];
+    const float2 d = make_float2(v[m].x - c.x - mu.x, v[m].y - c.y - mu.y);
+    v[m] = n < nmax ? cscale(d, c.z) : make_float2(0.f, 0.f);
+  }
+  team_fft_pre<NR>(v, my, t, tb, Sync{});                   // :205 fft(., Nr, 1)
+  if (valid) {
+#pragma unroll
+    for (int m = 0; m < P; ++m) st_c(o, t + T * m, cscale(v[m], cube_scale));    // :207
+  }
+}
+
+// ---------------------------------------------------------------------------
 // doppler_tile: RB = 256/T rows [r0, r0+RB) of one frame (K2 body, 256 threads).
 // Thread (b, u) = (tid % RB, tid / RB) is member u of row b's Nd-point team.
 // ---------------------------------------------------------------------------

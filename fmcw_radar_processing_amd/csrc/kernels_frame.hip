@@ -28,16 +28,38 @@ namespace fmcw {
 // chirp; a 256-thread workgroup holds 256/T teams; each team walks `cpt`
 // consecutive chirps.  Thread t loads samples t + T*m (coalesced), keeps them
 // in registers through the FFT and stores range bins t + T*m (coalesced).
+//
+// Streaming: the {cal, IF*w} taps sit in LDS (loaded once per workgroup) and
+// the twiddles of a chirp are loaded before the NEXT chirp's samples are
+// requested, so while chirp c is transformed the loads of chirp c+1 are in
+// flight (vmcnt completes in order: nothing issued after them is waited on).
 // ---------------------------------------------------------------------------
-template <int NR, typename TIn, typename TCube, bool PROFILE, bool PAIR>
+template <int NR, typename TIn, typename TCube, bool PROFILE>
 __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
   using Plan = FftPlan<NR>;
   constexpr int P = Plan::P, T = Plan::T;
   constexpr int TEAMS = T >= 256 ? 1 : 256 / T;
   constexpr int LDSN = Plan::STRIDE > 0 ? Plan::STRIDE : 1;
-  static_assert(!PAIR || (T % 2 == 0 && P % 2 == 0), "pair access needs an even team");
   __shared__ float2 lds[TEAMS * LDSN];
   __shared__ float2 red[TEAMS * (T > 64 ? T / 64 : 1)];
+  __shared__ float4 taps[NR];
+
+  const int nmax = a.S < NR ? a.S : NR;
+  {
+    constexpr int TP = (NR + 255) / 256;                       // taps per thread, loads issued together
+    float4 tp[TP];
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      tp[j] = a.calw[i < nmax ? i : 0];
+    }
+#pragma unroll
+    for (int j = 0; j < TP; ++j) {
+      const int i = threadIdx.x + 256 * j;
+      if (i < nmax) taps[i] = tp[j];
+    }
+  }
+  __syncthreads();
 
   const int team = threadIdx.x / T, t0 = threadIdx.x % T;
   float2* my = lds + team * LDSN;
@@ -50,21 +72,29 @@ __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
 #pragma unroll
   for (int m = 0; m < (PROFILE ? P : 1); ++m) pm[m] = 0.f;
 
+  float2 cur[P];
+  chirp_load<NR>(in + (g0 < a.nchirps ? g0 : 0) * a.S, g0 < a.nchirps, nmax, t0, cur);
   for (int c = 0; c < a.cpt; ++c) {
     const int64_t g = g0 + c;
     const bool valid = g < a.nchirps;
     // Opaque copy of the lane index: stops the compiler hoisting the per-lane
-    // LDS addresses and twiddles of every pass out of the chirp loop (that
-    // hoisting costs ~100 VGPRs and halves occupancy).
+    // LDS addresses and twiddle products of every pass out of the chirp loop
+    // (that hoisting costs ~100 VGPRs and halves occupancy).
     int t = t0;
     asm volatile("" : "+v"(t));
-    float2 v[P];
-    range_team<NR, PAIR>(in + (valid ? g : 0) * a.S, valid, out + g * NR, a.S, a.calw, a.cal_sum, a.if_scale, a.cube_scale,
-                         a.tw, my, myred, t, v);
+    float2 tb[FftPasses<NR>::NB];
+    load_tw_bases<NR>(tb, t, a.tw);                            // before the prefetch below
+    const bool vn = (c + 1 < a.cpt) && (g + 1 < a.nchirps);
+    float2 nxt[P];
+    chirp_load<NR>(in + (vn ? g + 1 : 0) * a.S, vn, nmax, t, nxt);
+    chirp_finish<NR>(cur, in + (valid ? g : 0) * a.S, valid, out + g * NR, a.S, taps, a.cal_sum, a.cube_scale, tb,
+                     my, myred, t);
     if constexpr (PROFILE) {
 #pragma unroll
-      for (int m = 0; m < P; ++m) pm[m] = fmaxf(pm[m], cabs2(v[m]));
+      for (int m = 0; m < P; ++m) pm[m] = fmaxf(pm[m], cabs2(cur[m]));
     }
+#pragma unroll
+    for (int m = 0; m < P; ++m) cur[m] = nxt[m];
   }
   if constexpr (PROFILE) {
     if (g0 >= a.nchirps) return;                               // :210 max over chirps
@@ -112,9 +142,7 @@ __global__ __launch_bounds__(256) void k_detect(DetectArgs a) {
 // ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
-// 16-byte "pair" global access (default) vs 8-byte per-lane access.  FMCW_PAIR=0
-// selects the latter; read at every launch so one process can A/B both.
-// 16-byte lane-pair access (FMCW_PAIR=1).  Off by default: on MI355X the
+// 16-byte lane-pair access in K2 (FMCW_PAIR=1).  Off by default: on MI355X the
 // 8-byte cyclic path measured slightly faster, and it shares the
 // fused kernel's summation order, so both schedules agree bit for bit.
 static bool pair_access_enabled() {
@@ -127,16 +155,8 @@ static hipError_t go_range(const RangeArgs& a, hipStream_t s) {
   constexpr int TEAMS = T >= 256 ? 1 : 256 / T;
   const int64_t per_block = (int64_t)TEAMS * a.cpt;
   const int64_t blocks = (a.nchirps + per_block - 1) / per_block;
-  // 16-byte (pair) access needs an even team and 16-byte-aligned chirp rows
-  constexpr bool kPairOk = (T % 2 == 0);
-  const bool pair = kPairOk && (a.S % 2 == 0) && pair_access_enabled();
-  if (a.profile) {
-    if (pair) hipLaunchKernelGGL((k_range<NR, TIn, TCube, true, kPairOk>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_range<NR, TIn, TCube, true, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  } else {
-    if (pair) hipLaunchKernelGGL((k_range<NR, TIn, TCube, false, kPairOk>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((k_range<NR, TIn, TCube, false, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
-  }
+  if (a.profile) hipLaunchKernelGGL((k_range<NR, TIn, TCube, true>), dim3((unsigned)blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_range<NR, TIn, TCube, false>), dim3((unsigned)blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

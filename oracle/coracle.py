@@ -34,7 +34,9 @@ def _p(a):
     return ct.c_void_p(0) if a is None else ct.c_void_p(a.ctypes.data)
 
 
-def process_frames(iq, cal, p, wr, wd, want_cube=False, want_rd=False, nthreads=0):
+def process_frames(iq, cal, p, wr, wd, want_cube=False, want_rd=False, nthreads=0, rd_out=None):
+    """rd_out: preallocated complex128 [F][nr][nd] that receives every row's
+    Doppler spectrum (no allocation per call; used by bench.py's CPU baseline)."""
     iq = np.ascontiguousarray(iq, np.complex64)
     F, C, S = iq.shape
     nr, nd, M = p["nr"], p["nd"], p["max_targets"]
@@ -42,6 +44,9 @@ def process_frames(iq, cal, p, wr, wd, want_cube=False, want_rd=False, nthreads=
                tgt_range_mag=np.zeros((F, M)), tgt_doppler_idx=np.zeros((F, M), np.int32), slow_mag=np.zeros((F, C)))
     cube = np.zeros((F, C, nr), np.complex128) if want_cube else None
     rd = np.zeros((F, nr, nd), np.complex128) if want_rd else None
+    if rd_out is not None:
+        assert rd_out.dtype == np.complex128 and rd_out.shape == (F, nr, nd) and rd_out.flags.c_contiguous
+        rd = rd_out
     c = np.ascontiguousarray(np.asarray(cal, np.complex128))
     wr = np.ascontiguousarray(wr, np.float64)
     wd = np.ascontiguousarray(wd, np.float64)

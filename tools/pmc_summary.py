@@ -1,6 +1,8 @@
 """Summarise rocprofv3 CSV output per kernel (development + profiles/ summaries).
 
-usage: python tools/pmc_summary.py <prof_dir>   (the -d directory of tools/profile_run.sh)
+usage: python tools/pmc_summary.py <prof_dir> [--json OUT --bench-log LOG]
+  (<prof_dir>: the -d directory of tools/profile_run.sh; --json writes the
+  per-kernel HBM traffic that bench.py reports as roofline.traffic)
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  On gfx950 FETCH_SIZE counts
 half the bytes of wide coalesced streaming reads (MI355X_MICROARCH.md, HBM):
 the 'fetch_x2' column applies that documented x2 correction.
@@ -27,14 +29,26 @@ def load_counters(path):
     return per, dur
 
 
-def main(d):
+LABELS = ("k_range", "k_doppler", "k_detect", "k_rd_fused", "k_compact", "k_stft_power", "k_stft_db")
+
+
+def label(k):
+    for lb in LABELS:
+        if k.startswith("fmcw::" + lb + "<") or k == "fmcw::" + lb:
+            return lb
+    return None
+
+
+def main(d, json_out=None, bench_log=None):
     rows = collections.OrderedDict()
+    stat_us = {}
     stats = os.path.join(d, "stats", "run_kernel_stats.csv")
     if os.path.exists(stats):
         print("== kernel stats (rocprofv3 --kernel-trace --stats) ==")
         print(f"{'kernel':72s} {'calls':>6s} {'avg_us':>9s} {'total_ms':>9s} {'pct':>6s}")
         with open(stats) as fh:
             for r in csv.DictReader(fh):
+                stat_us[short(r['Name'])] = (float(r['AverageNs']) / 1e3, int(r['Calls']))
                 print(f"{short(r['Name']):72s} {int(r['Calls']):6d} {float(r['AverageNs'])/1e3:9.2f} "
                       f"{float(r['TotalDurationNs'])/1e6:9.2f} {float(r['Percentage']):6.2f}")
     for sub in ("fetch", "write", "sq", "tcc"):
@@ -67,7 +81,40 @@ def main(d):
             if "GRBM_GUI_ACTIVE" in r:
                 parts.append(f"gui_active {r['GRBM_GUI_ACTIVE']:.0f}")
             print(f"{k:72s} " + " | ".join(parts))
+    if json_out:
+        import json
+        bench = {}
+        if bench_log and os.path.exists(bench_log):
+            for line in open(bench_log):
+                if line.startswith("{") and '"metric"' in line:
+                    bench = json.loads(line)
+        out = {"prof_dir": d, "bench_line": {k: bench.get(k) for k in ("value", "ms_per_step", "dtype", "config")},
+               "note": "hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) per dispatch; FETCH_SIZE x2 is the "
+                       "gfx950 correction of MI355X_MICROARCH.md (HBM section); separate --pmc passes",
+               "kernels": {}}
+        for k, r in rows.items():
+            lb = label(k)
+            if not lb or "FETCH_SIZE" not in r or "WRITE_SIZE" not in r:
+                continue
+            e = {"name": k, "fetch_kib": round(r["FETCH_SIZE"], 1), "write_kib": round(r["WRITE_SIZE"], 1),
+                 "hbm_bytes_per_launch": int((2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024)}
+            if k in stat_us:
+                e["rocprof_avg_us"], e["rocprof_calls"] = round(stat_us[k][0], 2), stat_us[k][1]
+            kb = (bench.get("kernels") or {}).get(lb)
+            if kb:
+                e["frames_per_launch"] = kb["frames_per_launch"]
+                e["bench_event_avg_us"] = kb["avg_launch_us"]
+            out["kernels"][lb] = e
+        with open(json_out, "w") as fh:
+            json.dump(out, fh, indent=1)
+        print(f"wrote {json_out}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--json")
+    ap.add_argument("--bench-log")
+    a = ap.parse_args()
+    main(a.dir, a.json, a.bench_log)
