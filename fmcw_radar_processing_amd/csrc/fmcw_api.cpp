@@ -68,7 +68,7 @@ struct DevBuf {
 
 size_t esize(int dtype) { return dtype == FMCW_C32H ? 4 : 8; }
 
-constexpr int kStages = 8;   // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call
+constexpr int kStages = 9;   // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call, 8 k_rd1p
 
 }  // namespace
 
@@ -94,6 +94,7 @@ struct fmcw_ctx {
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO, pipe_nslot = 2;
   DevBuf fused_ctrl, fused_slots, fused_rd_slots, fused_sticky;
+  DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
   bool fused_ran = false;
   int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
   struct Pending {
@@ -325,7 +326,7 @@ int fmcw_set_chunk_frames(fmcw_ctx* c, int64_t frames) {
 
 int fmcw_set_pipeline(fmcw_ctx* c, int32_t mode, int32_t nslot) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
-  if (mode < FMCW_PIPE_AUTO || mode > FMCW_PIPE_FUSED) return fail(FMCW_E_ARG, "bad pipeline mode");
+  if (mode < FMCW_PIPE_AUTO || mode > FMCW_PIPE_ONEPASS) return fail(FMCW_E_ARG, "bad pipeline mode");
   if (nslot != 0 && (nslot < 2 || nslot > 8)) return fail(FMCW_E_ARG, "nslot must be 0 or in [2, 8]");
   c->pipe_mode = mode;
   c->pipe_nslot = nslot == 0 ? 2 : nslot;
@@ -445,6 +446,80 @@ static int process_fused(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, in
   return FMCW_OK;
 }
 
+// Single-pass schedule (kernels_onepass.hip): k_rd1p computes range FFT,
+// profile, Doppler FFT and the per-row Doppler peaks of each frame without a
+// range cube; k_detect_1p runs the detection; k_slow_fix recomputes the rare
+// slow-time row that was not among a tile's candidates.  Chunks bound the
+// candidate scratch (OP_TILES*OP_CAND rows of PN floats per frame).
+static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int64_t F, float* d_prof,
+                           int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
+                           void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
+  const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
+  const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : 8192);
+  constexpr int TC = fmcw::OP_TILES * fmcw::OP_CAND;
+  CHK(c->op_rowpk.ensure((size_t)chunk * NR * 8));
+  CHK(c->op_cidx.ensure((size_t)chunk * TC * 4));
+  CHK(c->op_crows.ensure((size_t)chunk * TC * C * 4));
+  CHK(c->op_fix.ensure((size_t)chunk * 4 + 16));
+  int32_t* fix_count = c->op_fix.as<int32_t>();
+  int32_t* fix_list = fix_count + 4;
+  const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
+  const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
+  StageTimer span(c, 7, s, 1);
+  for (int64_t f0 = 0; f0 < F; f0 += chunk) {
+    const int64_t nf = std::min(chunk, F - f0);
+    fmcw::OnePassArgs a{};
+    a.iq = static_cast<const float2*>(d_iq) + (size_t)f0 * C * S;
+    a.F = nf; a.C = C; a.S = S;
+    a.calw = c->calw.as<float4>();
+    a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
+    a.rd = d_rd ? static_cast<float2*>(d_rd) + (size_t)f0 * NR * ND : nullptr;
+    a.profile = d_prof + f0 * NR;
+    a.rowpk = c->op_rowpk.as<int2>();
+    a.cand_idx = c->op_cidx.as<int32_t>();
+    a.cand_rows = c->op_crows.as<float>();
+    a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
+    a.probe_frame = (pframe >= f0 && pframe < f0 + nf) ? pframe - f0 : -1;
+    a.probe_chirp = pchirp;
+    a.probe_mag = d_probe;
+    {
+      const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
+      a.force_fix = (e && e[0] == '1') ? 1 : 0;
+    }
+    {
+      StageTimer tm(c, 8, s, 2);
+      HIPCHK(fmcw::launch_onepass(a, s));
+      tm.done();
+    }
+    HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
+    fmcw::Detect1pArgs k{};
+    k.profile = a.profile; k.rowpk = a.rowpk; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
+    k.nframes = (int)nf; k.NR = NR; k.C = C; k.M = M;
+    k.det.ND = ND; k.det.C = C; k.det.M = M;
+    k.det.range_thr = p->range_thr; k.det.doppler_thr = p->doppler_thr;
+    k.det.min_d = p->min_d; k.det.max_d = p->max_d; k.det.dist_per_bin = p->dist_per_bin;
+    k.det.fallback = p->doppler_fallback_idx;
+    k.det.cube_unscale = 1.0f; k.det.rd_unscale = 1.0f;
+    k.count = d_count + f0; k.ridx = d_ridx + f0 * M; k.rmag = d_rmag + f0 * M; k.didx = d_didx + f0 * M;
+    k.slow_mag = d_slow + f0 * C;
+    k.fix_list = fix_list; k.fix_count = fix_count;
+    {
+      StageTimer tm(c, 2, s, 2);
+      HIPCHK(fmcw::launch_detect_1p(k, s));
+      tm.done();
+    }
+    fmcw::SlowFixArgs x{};
+    x.iq = a.iq; x.C = C; x.S = S; x.NR = NR;
+    x.calw = a.calw; x.tw_nr = a.tw_nr;
+    x.ridx = k.ridx; x.M = M;
+    x.fix_list = fix_list; x.fix_count = fix_count;
+    x.slow_mag = k.slow_mag;
+    HIPCHK(fmcw::launch_slow_fix(x, s));
+  }
+  span.done();
+  return FMCW_OK;
+}
+
 int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
                         float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
                         float* d_slow, void* d_cube, void* d_rd, int32_t out_dtype, int64_t probe_column,
@@ -459,6 +534,15 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
   if (probe_column < 0 || probe_column > F * (int64_t)C) return fail(FMCW_E_ARG, "probe_column out of range");
   hipStream_t s = pick(c, stream);
+  const bool onepass_ok = !d_cube && in_dtype == FMCW_C64 && (!d_rd || out_dtype == FMCW_C64) &&
+                          fmcw::onepass_supported(S, C, NR, ND);
+  if (c->pipe_mode == FMCW_PIPE_ONEPASS) {
+    if (!onepass_ok)
+      return fail(FMCW_E_ARG, "single-pass schedule: needs nr 1024, pn == nd == 256, even nts <= nr, "
+                              "complex64 in/out and no range cube");
+    return process_onepass(c, p, d_iq, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd, probe_column,
+                           d_probe, s);
+  }
   const bool fusable = !d_cube && fmcw::fused_supported(NR, ND);
   if (c->pipe_mode == FMCW_PIPE_FUSED && !fusable)
     return fail(FMCW_E_ARG, "fused schedule: no fused kernel for this geometry, or a range cube was requested");

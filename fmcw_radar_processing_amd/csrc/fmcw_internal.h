@@ -98,6 +98,66 @@ struct FusedArgs {
 
 inline int64_t fused_ctrl_words(int64_t F) { return 256 + 3 * F + 1; }
 
+// Single-pass range+Doppler (kernels_onepass.hip).  Frame f is split into
+// OP_TILES range tiles: tile t owns the bins r == t (mod OP_TILES) for every
+// chirp, held in registers; the range cube never exists in memory.
+constexpr int OP_TILES = 8;
+constexpr int OP_CAND = 2;           // slow-time candidate rows kept per tile
+
+struct OnePassArgs {
+  const float2* iq;        // [F][C][S] c64
+  int64_t F;
+  int C, S;                // NR = 1024, ND = C (kernel template)
+  const float4* calw;      // [S] {cal.re, cal.im, IF_scale*w, w}
+  const float2* tw_nr;     // [NR]
+  const float2* tw_nd;     // [ND]
+  const float* wd;         // [C]
+  float2* rd;              // [F][NR][ND] or nullptr (then only the row peaks are kept)
+  float* profile;          // [F][NR]
+  int2* rowpk;             // [F][NR] {float bits of max_d |D[r,d]|, first argmax d (fftshift-ed, 0-based)}
+  int32_t* cand_idx;       // [F][OP_TILES][OP_CAND] 0-based bin or -1
+  float* cand_rows;        // [F][OP_TILES][OP_CAND][C] |X[bin, k]|
+  float range_thr, min_d, max_d, dist_per_bin;
+  int64_t probe_frame;     // frame within this launch, -1 = none
+  int probe_chirp;
+  float* probe_mag;        // [NR]
+  int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
+                           // slow-time row goes through k_slow_fix
+};
+
+struct Detect1pArgs {
+  const float* profile;    // [F][NR]
+  const int2* rowpk;       // [F][NR]
+  const int32_t* cand_idx; // [F][OP_TILES][OP_CAND]
+  const float* cand_rows;  // [F][OP_TILES][OP_CAND][C]
+  int nframes, NR, C, M;
+  DetectParams det;
+  int32_t* count;
+  int32_t* ridx;
+  float* rmag;
+  int32_t* didx;
+  float* slow_mag;         // [F][C]
+  int32_t* fix_list;       // [F] frames whose slow row must be recomputed
+  int32_t* fix_count;      // device scalar (zeroed by the caller)
+};
+
+struct SlowFixArgs {
+  const float2* iq;        // [F][C][S]
+  int C, S, NR;
+  const float4* calw;
+  const float2* tw_nr;
+  const int32_t* ridx;     // [F][M]
+  int M;
+  const int32_t* fix_list;
+  const int32_t* fix_count;
+  float* slow_mag;
+};
+
+hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s);
+hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s);
+hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s);
+bool onepass_supported(int nts, int pn, int nr, int nd);
+
 struct StftArgs {
   const float* slow_mag;   // [*][pn]
   const int32_t* frame_list;

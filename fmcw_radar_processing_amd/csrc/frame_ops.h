@@ -347,20 +347,16 @@ __device__ __forceinline__ void wave_argmax(float& v, int& i) {
   }
 }
 
-// Latency-shaped: every load a lane needs in a phase is issued together
-// (profile + both neighbours; then the target's Doppler row and slow-time
-// row), so a frame costs two dependent memory round trips.
-template <int NR, bool NT, typename TRd, typename TCube>
-__device__ __forceinline__ void detect_frame(const DetectParams& a, int lane, const float* __restrict__ prof,
-                                             const TRd* __restrict__ rd, const TCube* __restrict__ cube,
-                                             int32_t* count, int32_t* ridx, float* rmag, int32_t* didx,
-                                             float* __restrict__ slow, bool probe, int probe_chirp,
-                                             float* __restrict__ probe_mag) {
+// f_search_peak (radar_processing.m:211; helper absent from the reference,
+// rule of SURVEY 8a a9): local maxima above range_thr inside [min_d, max_d];
+// the max_targets largest, ties -> lower index.  One wave; every lane ends
+// with the same sel[0..n-1] (0-based bins) and their magnitudes.
+template <int NR, bool NT>
+__device__ __forceinline__ int select_peaks(const DetectParams& a, int lane, const float* __restrict__ prof,
+                                            int (&sel)[8], float (&selv)[8]) {
   constexpr int PPL = NR >= 64 ? NR / 64 : 1;
-  const int ND = a.ND, C = a.C, M = a.M;
+  const int M = a.M;
   const double dpb = a.dist_per_bin, lo = a.min_d, hi = a.max_d;
-  // f_search_peak: local maxima above range_thr inside
-  // [min_d, max_d]; the max_targets largest, ties -> lower index.
   float cv[PPL];
 #pragma unroll
   for (int j = 0; j < PPL; ++j) {
@@ -373,8 +369,6 @@ __device__ __forceinline__ void detect_frame(const DetectParams& a, int lane, co
     }
     cv[j] = v;
   }
-  int sel[8];
-  float selv[8];
   int n = 0;
 #pragma unroll
   for (int q = 0; q < 8; ++q) { sel[q] = -1; selv[q] = 0.f; }
@@ -394,6 +388,22 @@ __device__ __forceinline__ void detect_frame(const DetectParams& a, int lane, co
       if (lane + 64 * j == bi) cv[j] = -1.f;            // exclude from the next round
     ++n;
   }
+  return n;
+}
+
+// Latency-shaped: every load a lane needs in a phase is issued together
+// (profile + both neighbours; then the target's Doppler row and slow-time
+// row), so a frame costs two dependent memory round trips.
+template <int NR, bool NT, typename TRd, typename TCube>
+__device__ __forceinline__ void detect_frame(const DetectParams& a, int lane, const float* __restrict__ prof,
+                                             const TRd* __restrict__ rd, const TCube* __restrict__ cube,
+                                             int32_t* count, int32_t* ridx, float* rmag, int32_t* didx,
+                                             float* __restrict__ slow, bool probe, int probe_chirp,
+                                             float* __restrict__ probe_mag) {
+  const int ND = a.ND, C = a.C, M = a.M;
+  int sel[8];
+  float selv[8];
+  const int n = select_peaks<NR, NT>(a, lane, prof, sel, selv);
   // :257-259 slow-time row of the strongest target, from the stored cube;
   // issued before the Doppler rows so both round trips overlap
   {

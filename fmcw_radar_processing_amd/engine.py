@@ -77,7 +77,7 @@ class Engine:
         check(self.lib.fmcw_set_chunk_frames(self.h, int(n)))
 
     def set_pipeline(self, mode: int, nslot: int = 0) -> None:
-        """FMCW_PIPE_AUTO / _STREAMS / _FUSED (include/fmcw.h); nslot cube slots per XCD."""
+        """FMCW_PIPE_AUTO / _STREAMS / _FUSED / _ONEPASS (include/fmcw.h); nslot cube slots per XCD."""
         check(self.lib.fmcw_set_pipeline(self.h, int(mode), int(nslot)))
 
     def pipeline_status(self) -> int:

@@ -204,7 +204,8 @@ int fmcw_synth_device(fmcw_ctx* ctx, const fmcw_params* p, int64_t frame0, int64
  * Doppler launch; the chunks run as a 3-stream software pipeline) and one pair
  * per STFT-side launch (stages 3-6); 2 = additionally one pair per K1/K2/K3.
  * stage: 0 range, 1 doppler, 2 detect, 3 compact, 4 stft_power, 5 stft_db,
- *        6 range_only, 7 range+Doppler span.  fmcw_timing_read synchronises. */
+ *        6 range_only, 7 range+Doppler span, 8 k_rd1p (single-pass schedule,
+ *        level 2).  fmcw_timing_read synchronises. */
 int fmcw_timing_enable(fmcw_ctx* ctx, int32_t enable);
 int fmcw_timing_read(fmcw_ctx* ctx, int32_t stage, double* total_ms, int64_t* launches);
 int fmcw_timing_reset(fmcw_ctx* ctx);
@@ -223,9 +224,15 @@ int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
  *  FMCW_PIPE_FUSED   one persistent kernel per call: each XCD runs its frames'
  *                    range, Doppler and detect items from a ticket queue, the
  *                    range cube of a frame stays in that XCD's L2.  E_ARG when
- *                    the geometry has no fused kernel or a cube is requested.
+ *                    the geometry has no fused kernel or a cube is requested;
+ *  FMCW_PIPE_ONEPASS single pass per frame (kernels_onepass.hip): 8 range tiles
+ *                    per frame, each keeping its bins (r == t mod 8) of every
+ *                    chirp in registers/LDS through the Doppler FFT, so the
+ *                    range cube never reaches memory.  Needs nr 1024,
+ *                    pn == nd == 256, even nts <= nr, complex64 in and out,
+ *                    no range cube (else E_ARG).
  * nslot (>= 2, 0 = default 2): cube slots per XCD for the fused schedule. */
-enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_FUSED = 2 };
+enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_FUSED = 2, FMCW_PIPE_ONEPASS = 3 };
 int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode, int32_t nslot);
 
 /* Fused-schedule health after the last call (synchronises the stream):
