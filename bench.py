@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU per step")
     ap.add_argument("--fp16", action="store_true", help="config-4 fp16 storage variant")
     ap.add_argument("--chunk", type=int, default=0, help="frames per range/Doppler chunk (0 = library default)")
-    ap.add_argument("--pipeline", choices=["auto", "streams", "fused"], default="auto",
+    ap.add_argument("--pipeline", choices=["auto", "streams", "fused", "onepass"], default="auto",
                     help="range/Doppler schedule (include/fmcw.h fmcw_set_pipeline)")
     ap.add_argument("--nslot", type=int, default=0, help="fused schedule: cube slots per XCD (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
@@ -75,7 +75,7 @@ def main():
     eng.set_taps(cfg, P.synth_calibration(S))
     if args.chunk:
         eng.set_chunk_frames(args.chunk)
-    eng.set_pipeline({"auto": 0, "streams": 1, "fused": 2}[args.pipeline], args.nslot)
+    eng.set_pipeline({"auto": 0, "streams": 1, "fused": 2, "onepass": 3}[args.pipeline], args.nslot)
     stream = torch.cuda.current_stream(dev)
 
     # ---- device-resident input + outputs ------------------------------------------
@@ -162,7 +162,9 @@ def main():
     alg_per_frame = C * S * esz + NR * ND * esz + NR * 4 + C * 4
     k1_per_frame = C * S * esz + C * NR * 8          # streams schedule keeps an fp32 cube
     kern = {}
+    # k_rd1p (single-pass schedule): input + RD map + profile, no cube
     for name, label, per_frame in (("range", "k_range", k1_per_frame), ("doppler", "k_doppler", C * NR * 8 + NR * ND * esz + NR * 4),
+                                   ("onepass", "k_rd1p", C * S * esz + NR * ND * esz + NR * 4),
                                    ("detect", "k_detect", None)):
         ms, n = stages.get(name, (0.0, 0))
         if n:
@@ -182,16 +184,19 @@ def main():
                 "span_us": round(per_launch_ms * 1e3, 2), "frames_per_span": fpl, "alg_bytes_per_frame": alg_per_frame,
                 "what": "range+Doppler span (before first k_range .. after last k_doppler), SURVEY 8d bytes"}
     pmc = load_pmc(os.path.join(ROOT, "profiles"), args)
-    if "k_range" in kern:
-        k = kern["k_range"]
+    dom = "k_rd1p" if "k_rd1p" in kern else "k_range"
+    if dom in kern:
+        k = kern[dom]
         traffic = None
-        if pmc and "k_range" in pmc.get("kernels", {}):
-            pk = pmc["kernels"]["k_range"]
+        if pmc and dom in pmc.get("kernels", {}):
+            pk = pmc["kernels"][dom]
             if abs(pk.get("frames_per_launch", 0) - k["frames_per_launch"]) < 0.5:
                 traffic = pk.get("hbm_bytes_per_launch")
         roof = {"bound": "hbm", "achieved": k["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(k["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": "k_range (K1: calibration, mean removal, window, 1024-pt range FFT, cube store)",
+                "kernel": ("k_rd1p (single pass: calibration, mean removal, window, range FFT, profile, Doppler FFT, "
+                           "RD store; one range tile of one frame per workgroup)") if dom == "k_rd1p" else
+                          "k_range (K1: calibration, mean removal, window, 1024-pt range FFT, cube store)",
                 "alg_bytes_per_launch": k["alg_bytes_per_launch"], "avg_launch_us": k["avg_launch_us"],
                 "frames_per_launch": k["frames_per_launch"],
                 "traffic_source": pmc.get("source") if pmc and traffic else None}

@@ -472,6 +472,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.iq = static_cast<const float2*>(d_iq) + (size_t)f0 * C * S;
     a.F = nf; a.C = C; a.S = S;
     a.calw = c->calw.as<float4>();
+    a.cal_mean = make_float2(c->cal_sum.x / S, c->cal_sum.y / S);
     a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
     a.rd = d_rd ? static_cast<float2*>(d_rd) + (size_t)f0 * NR * ND : nullptr;
     a.profile = d_prof + f0 * NR;

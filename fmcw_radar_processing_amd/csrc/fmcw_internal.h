@@ -109,6 +109,7 @@ struct OnePassArgs {
   int64_t F;
   int C, S;                // NR = 1024, ND = C (kernel template)
   const float4* calw;      // [S] {cal.re, cal.im, IF_scale*w, w}
+  float2 cal_mean;         // mean(cal) over the S samples (linearity form of :203-204)
   const float2* tw_nr;     // [NR]
   const float2* tw_nd;     // [ND]
   const float* wd;         // [C]

@@ -4,8 +4,9 @@
 // The two-pass schedule (k_range -> cube in HBM -> k_doppler) moves 8.4 MB per
 // config-3 frame for 4.2 MB of algorithmic traffic.  Here a frame is split into
 // OP_TILES = 8 range tiles; the workgroup of tile t computes only the bins
-// r == t (mod 8), for every chirp, and keeps them in VGPRs until its Doppler
-// FFTs are done.  Decimation in frequency makes the partial range FFT cheap:
+// r == t (mod 8), for every chirp, and keeps them on chip (half in VGPRs, half
+// in LDS) until its Doppler FFTs are done.  Decimation in frequency makes the
+// partial range FFT cheap:
 //
 //   n = a + 128 b (a < 128, b < 8),  r = t + 8 m (m < 128):
 //   X[t + 8m] = sum_a W128^(a m) * [ W1024^(a t) * sum_b y[a + 128 b] W8^(b t) ]
@@ -15,20 +16,31 @@
 // 7 from the XCD's L2.  Blocks b and b+8 share an XCD, so the 8 tiles of a
 // frame are blocks 64j + 8t + x (same x): dispatched together, same L2.
 //
+// Calibration and mean removal (:203-204) enter by linearity.  With
+// y[n] = (x[n] - cal[n] - mu) w'[n] (w' = IF_scale * 2 blackman, :205) and
+// mu = mean(x) - mean(cal):
+//   stage A = sum_b x w' W8^(bt) - G_t[a] - mean(x) H_t[a],
+//   G_t[a] = sum_b (cal - mean(cal)) w' W8^(bt),  H_t[a] = sum_b w' W8^(bt),
+// two per-lane constants per sub-sequence (built once per workgroup, in LDS),
+// so a chirp is consumed straight from its loads: no calibrated copy, and the
+// chirp mean is one wave sum that is applied after stage A.
+//
 // Per chirp (one wave, 16 samples per lane as 8 float4 loads, lane l holds
-// a = 2l and 2l+1):   :203-204 calibration + IF scale + mean removal (xor
-// butterfly wave sum: every lane gets the same mean), :205 window, stage A,
-// a 64-point cross-lane DIF FFT on each of the two sub-sequences (DPP and
-// v_permlane16/32_swap exchanges, no LDS), one in-lane radix-2 -> bins
-// r(l, s) = t + 8 (bitrev6(l) + 64 s), s = 0, 1.
-// Wave w handles chirps k = w + 16 k2 (k2 < 16): VGPR tile[k2][s].
+// a = 2l and 2l+1): stage A as the float4s arrive (the next chirp's first half
+// is requested as soon as this chirp's first half is consumed: a rolling
+// prefetch that keeps >= 4 loads per lane in flight in 32 VGPRs), the mean
+// correction, a 64-point cross-lane DIF FFT on each of the two sub-sequences
+// (DPP and v_permlane16/32_swap exchanges, no LDS), one in-lane radix-2 ->
+// bins r(l, s) = t + 8 (bitrev6(l) + 64 s), s = 0, 1.
+// Wave w handles chirps k = w + 16 k2 (k2 < 16): slot 0 in VGPRs, slot 1 in LDS.
 //
 // Doppler (:216-219) for every row of the tile: the mean over chirps and the
 // max-abs profile (:210, :265) are reduced across waves in LDS; each lane runs
 // a 16-point DFT over its own chirps (k2), twiddles by W256^(w d2), and the
-// last 16-point DFT over the waves goes through an LDS corner turn, one slot
-// (64 rows) at a time; fftshift is folded into the store index.  Each row's
-// max |D| and its first argmax (:233) are kept so detection never reads RD.
+// last 16-point DFT over the waves goes through an XOR-swizzled LDS corner
+// turn (the slot-1 region, 128 KiB), one slot (64 rows) at a time; fftshift
+// is folded into the store index.  Each row's max |D| and its first argmax
+// (:233) are kept so detection never reads RD.
 //
 // Slow-time row (:257-259): the target bin is only known once all 8 tiles'
 // profiles exist, so each tile stores |X[r, :]| for its OP_CAND strongest
@@ -41,7 +53,7 @@ namespace fmcw {
 namespace op {
 
 constexpr int NR = 1024;
-constexpr int NW = 16;                 // waves per workgroup
+constexpr int NW = 8;                  // waves per workgroup (2 per SIMD: 256 VGPRs per lane)
 static_assert(NR / OP_TILES == 128, "the lane layout assumes a 128-point sub-FFT");
 
 using c2 = f2v;                        // complex (re, im) in a packed-fp32 register pair
@@ -113,46 +125,68 @@ __device__ __forceinline__ c2 dif_stage(c2 x, int lane, c2 tw, float sg) {
   return H == 1 ? u : cmv(u, tw);
 }
 
+// Wave-uniform table read through the constant address space: an s_load into
+// SGPRs instead of a vector load into VGPRs (the index must be wave-uniform).
+__device__ __forceinline__ float sload(const float* p, int i) {
+  return ((const __attribute__((address_space(4))) float*)p)[i];
+}
+__device__ __forceinline__ float2 sload(const float2* p, int i) {
+  const f2v v = ((const __attribute__((address_space(4))) f2v*)p)[i];
+  return make_float2(v.x, v.y);
+}
+
 __device__ __forceinline__ int bitrev6(int l) { return (int)(__brev((unsigned)l) >> 26); }
 
-// LDS image of k_rd1p (bytes).  Range phase: [tile slot 1 | taps | red1];
-// Doppler phase: the corner turn reuses [tile slot 1 | taps].
-template <int CPW> struct Lds1p {
-  static constexpr int C = NW * CPW;
-  static constexpr int T1 = C * 64 * 8;                 // slot-1 tile: [chirp][lane] c2
-  static constexpr int TC = (NR / 2) * 16;              // {cal pair} per sample pair
-  static constexpr int TW = (NR / 2) * 8;               // {IF*w pair}
-  static constexpr int RED = NW * 64 * 12;              // {sum.re, sum.im, max|X|^2} per (wave, lane)
-  static constexpr int SROW = CPW + 1;                  // corner-turn row pitch (c2): conflict-free
-  static constexpr int STG = NW * 64 * SROW * 8;
-  static constexpr int OFF_TC = T1, OFF_TW = T1 + TC, OFF_RED1 = T1 + TC + TW;
-  static constexpr int BYTES = OFF_RED1 + RED;
-  static_assert(STG <= OFF_RED1, "corner turn must fit in the slot-1 tile + taps region");
-  static_assert(RED <= TC + TW, "slot-0 reduction reuses the taps region");
+
+// 32-point forward DFT in registers (natural order): radix-2 over two dft<16>.
+__device__ __forceinline__ void dft32(float2 (&v)[32]) {
+  constexpr float kc[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                            0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                            0.19509032201612826785f, 0.0f, -0.19509032201612826785f, -0.38268343236508977173f,
+                            -0.55557023301960222474f, -0.70710678118654752440f, -0.83146961230254523708f,
+                            -0.92387953251128675613f, -0.98078528040323044913f};
+  constexpr float ks[16] = {0.0f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
+                            0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
+                            0.98078528040323044913f, 1.0f, 0.98078528040323044913f, 0.92387953251128675613f,
+                            0.83146961230254523708f, 0.70710678118654752440f, 0.55557023301960222474f,
+                            0.38268343236508977173f, 0.19509032201612826785f};
+  float2 e[16], o[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    e[i] = v[2 * i];
+    o[i] = v[2 * i + 1];
+  }
+  dft<16>(e);
+  dft<16>(o);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float2 ot = k == 0 ? o[0] : cmul(o[k], make_float2(kc[k], -ks[k]));   // W32^k
+    v[k] = cadd(e[k], ot);
+    v[k + 16] = csub(e[k], ot);
+  }
+}
+
+// LDS image of k_rd1p.
+struct Lds1p {
+  c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the reduction scratch; then the corner turn
+  c2 w[8 * 64];            // {w'[2l + 128j], w'[2l + 1 + 128j]} at [j][l]
+  c2 g[128], h[128];       // G'_t[a], H'_t[a] (times W1024^(a t))
+  c2 mu[2][64];
+  float prof[2][64];
+  int cand[OP_CAND];
 };
 
 }  // namespace op
 
 // ---------------------------------------------------------------------------
-// k_rd1p: one workgroup (16 waves) = one range tile of one frame.
-// FULL: S == NR (no zero padding, no masking).
+// k_rd1p: one workgroup (8 waves, 2 per SIMD, 256 VGPRs per lane) = one range
+// tile of one frame.  FULL: S == NR (no zero padding, no masking).
 // ---------------------------------------------------------------------------
-template <int CPW, bool FULL>
-__global__ __launch_bounds__(1024, 1) void k_rd1p(OnePassArgs a) {
+template <bool FULL>
+__global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   using namespace op;
-  using L = Lds1p<CPW>;
-  constexpr int ND = NW * CPW, C = ND, SROW = L::SROW;
-  static_assert(CPW == 16, "corner turn written for 16 chirps per wave (ND = PN = 256)");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[L::BYTES];
-  __shared__ c2 s_mu[2][64];
-  __shared__ float s_prof[2][64];
-  __shared__ int s_cand[OP_CAND];
-  c2* s_t1 = reinterpret_cast<c2*>(smem);
-  f4v* s_tc = reinterpret_cast<f4v*>(smem + L::OFF_TC);
-  c2* s_tw = reinterpret_cast<c2*>(smem + L::OFF_TW);
-  float* red0 = reinterpret_cast<float*>(smem + L::OFF_TC);
-  float* red1 = reinterpret_cast<float*>(smem + L::OFF_RED1);
-  c2* s_stg = reinterpret_cast<c2*>(smem);
+  constexpr int CPW = 32, C = NW * CPW, ND = C;  // wave w owns chirps w + 8 k2, k2 < 32
+  __shared__ __attribute__((aligned(16))) Lds1p L;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: scalar loads / SGPRs
@@ -162,81 +196,97 @@ __global__ __launch_bounds__(1024, 1) void k_rd1p(OnePassArgs a) {
   if (f >= a.F) return;                          // block-uniform
   const int S = FULL ? NR : a.S;
 
-  if (tid < NR / 2) {
-    const int n0 = 2 * tid;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 c0 = n0 < S ? a.calw[n0] : z4, c1 = n0 + 1 < S ? a.calw[n0 + 1] : z4;
-    s_tc[tid] = f4v{c0.x, c0.y, c1.x, c1.y};
-    s_tw[tid] = c2{c0.z, c1.z};                  // 0 beyond S: fft(., Nr) zero-padding
+  // ---- per-workgroup tables: window pairs, G'/H' (linearity constants) ----
+  {
+    const int n0 = 2 * lane + 128 * w;           // (j, l) = (w, lane)
+    L.w[tid] = c2{n0 < S ? a.calw[n0].z : 0.f, n0 + 1 < S ? a.calw[n0 + 1].z : 0.f};
+  }
+  if (tid < 128) {                               // a = tid
+    c2 g = c2{0.f, 0.f}, h = c2{0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = tid + 128 * j;
+      if (n < S) {
+        const float4 cw = a.calw[n];
+        const c2 c8 = tov(sload(a.tw_nr, (128 * j * t) & (NR - 1)));
+        const c2 cc = c2{cw.x - a.cal_mean.x, cw.y - a.cal_mean.y} * cw.z;
+        g = cmacv(g, cc, c8, c2{-c8.y, c8.x});
+        h = __builtin_elementwise_fma(c2{cw.z, cw.z}, c8, h);
+      }
+    }
+    const c2 ta = tov(a.tw_nr[(tid * t) & (NR - 1)]);
+    L.g[tid] = cmv(g, ta);
+    L.h[tid] = cmv(h, ta);
   }
 
   // per-lane / per-tile twiddles (all from the float64-rounded table)
   const c2 twa0 = tov(a.tw_nr[(2 * lane * t) & (NR - 1)]);
   const c2 twa1 = tov(a.tw_nr[((2 * lane + 1) * t) & (NR - 1)]);
-  c2 w8[8], w8s[8];                              // W8^(j t): wave-uniform
+  c2 w8[8], w8s[8];                              // W8^(j t): wave-uniform (SGPRs)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    w8[j] = tov(a.tw_nr[(128 * j * t) & (NR - 1)]);
+    w8[j] = tov(sload(a.tw_nr, (128 * j * t) & (NR - 1)));
     w8s[j] = c2{-w8[j].y, w8[j].x};
   }
   c2 twh[5];                                     // spans 32, 16, 8, 4, 2 (1 on clear lanes)
   float sg[6];                                   // spans 32 .. 1
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    const int h = 32 >> i;
-    sg[i] = (lane & h) ? -1.f : 1.f;
-    if (i < 5) twh[i] = (lane & h) ? tov(a.tw_nr[((lane & (h - 1)) * (512 / h)) & (NR - 1)]) : c2{1.f, 0.f};
+    const int hh = 32 >> i;
+    sg[i] = (lane & hh) ? -1.f : 1.f;
+    if (i < 5) twh[i] = (lane & hh) ? tov(a.tw_nr[((lane & (hh - 1)) * (512 / hh)) & (NR - 1)]) : c2{1.f, 0.f};
   }
   const int m0 = bitrev6(lane);
   const c2 w128 = tov(a.tw_nr[8 * m0]);
   const int r0 = t + 8 * m0, r1 = r0 + 512;      // this lane's two range bins
   __syncthreads();
 
-  // ---------------- range phase: :203-205 for chirps w + 16 k2 -------------
-  const float2* __restrict__ fr = a.iq + f * (int64_t)C * S;
+  // ---------------- range phase: :203-205 for chirps w + 8 k2 --------------
+  const f4v* __restrict__ fr = reinterpret_cast<const f4v*>(a.iq + f * (int64_t)C * S);
+  const int S2 = S >> 1;                         // float4 (sample pairs) per chirp
   const float invS = 1.0f / (float)S;
-  c2 tile0[CPW];                                  // slot 1 goes to LDS (s_t1)
-  float pm0 = 0.f, pm1 = 0.f;
-  c2 ms0 = c2{0.f, 0.f}, ms1 = c2{0.f, 0.f};
-#pragma unroll
-  for (int k2 = 0; k2 < CPW; ++k2) {
-    const int k = w + NW * k2;
-    const f4v* __restrict__ xq = reinterpret_cast<const f4v*>(fr + (int64_t)k * S);
-    f4v xv[8];
+  auto ld_chirp = [&](int k, f4v (&x)[8]) {
+    const f4v* __restrict__ q = fr + (int64_t)k * S2;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int p = lane + 64 * j;               // sample pair: samples 2p, 2p+1
-      if constexpr (FULL) xv[j] = (xq + 64 * j)[lane];   // scalar base per j, one lane offset
-      else xv[j] = xq[2 * p < S ? p : 0];
+      if constexpr (FULL) x[j] = (q + 64 * j)[lane];
+      else x[j] = q[p < S2 ? p : 0];
     }
-    c2 d[16];
-    c2 s = c2{0.f, 0.f};
+  };
+  float2 tile0[CPW];                             // slot 1 goes to LDS (L.t1)
+  f4v buf[3][8];                                 // chirp ring: 2 chirps in flight while one is consumed
+  ld_chirp(w, buf[0]);
+  ld_chirp(w + NW, buf[1]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f4v c = s_tc[lane + 64 * j];
-      d[2 * j] = xv[j].xy - c.xy;                // :203 (x - calib_rx1)
-      d[2 * j + 1] = xv[j].zw - c.zw;
-      if (!FULL && !(2 * (lane + 64 * j) < S)) d[2 * j] = d[2 * j + 1] = c2{0.f, 0.f};
-      s += d[2 * j] + d[2 * j + 1];
-    }
-    // :204 mean over the S samples (IF_scale is folded into the taps)
-    const c2 mu = c2{wave_sum(s.x), wave_sum(s.y)} * invS;
-    c2 A0, A1;
+  for (int k2 = 0; k2 < CPW; ++k2) {
+    const int k = w + NW * k2;
+    if (k2 + 2 < CPW) ld_chirp(k + 2 * NW, buf[(k2 + 2) % 3]);
+    const f4v (&x)[8] = buf[k2 % 3];
+    c2 B0, B1, sx = c2{0.f, 0.f};
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const c2 sw = s_tw[lane + 64 * j];
-      const c2 y0 = (d[2 * j] - mu) * sw.xx;     // :205 .* (IF_scale * 2*blackman)
-      const c2 y1 = (d[2 * j + 1] - mu) * sw.yy;
+    for (int j = 0; j < 8; ++j) {                // stage A straight from the loads
+      f4v v = x[j];
+      if constexpr (!FULL)
+        if (!(lane + 64 * j < S2)) v = f4v{0.f, 0.f, 0.f, 0.f};
+      const c2 wv = L.w[j * 64 + lane];
+      const c2 z0 = v.xy * wv.x, z1 = v.zw * wv.y;    // x .* (IF_scale * 2 blackman)
+      sx += v.xy + v.zw;
       if (j == 0) {
-        A0 = y0;
-        A1 = y1;
-      } else {                                   // stage A: sum_b y[a + 128 b] W8^(b t)
-        A0 = cmacv(A0, y0, w8[j], w8s[j]);
-        A1 = cmacv(A1, y1, w8[j], w8s[j]);
+        B0 = z0;
+        B1 = z1;
+      } else {                                   // sum_b y[a + 128 b] W8^(b t)
+        B0 = cmacv(B0, z0, w8[j], w8s[j]);
+        B1 = cmacv(B1, z1, w8[j], w8s[j]);
       }
     }
-    A0 = cmv(A0, twa0);                          // * W1024^(a t)
-    A1 = cmv(A1, twa1);
+    // :204 mean over the S samples, applied after stage A (linearity)
+    const c2 mx = c2{wave_sum(sx.x), wave_sum(sx.y)} * invS;
+    const c2 mxs = c2{-mx.y, mx.x};
+    const f4v g = reinterpret_cast<const f4v*>(L.g)[lane];
+    const f4v h = reinterpret_cast<const f4v*>(L.h)[lane];
+    c2 A0 = cmv(B0, twa0) - cmacv(g.xy, h.xy, mx, mxs);   // * W1024^(a t), - G' - mean(x) H'
+    c2 A1 = cmv(B1, twa1) - cmacv(g.zw, h.zw, mx, mxs);
     A0 = dif_stage<32>(A0, lane, twh[0], sg[0]); A1 = dif_stage<32>(A1, lane, twh[0], sg[0]);
     A0 = dif_stage<16>(A0, lane, twh[1], sg[1]); A1 = dif_stage<16>(A1, lane, twh[1], sg[1]);
     A0 = dif_stage<8>(A0, lane, twh[2], sg[2]);  A1 = dif_stage<8>(A1, lane, twh[2], sg[2]);
@@ -245,48 +295,62 @@ __global__ __launch_bounds__(1024, 1) void k_rd1p(OnePassArgs a) {
     A0 = dif_stage<1>(A0, lane, twh[4], sg[5]);  A1 = dif_stage<1>(A1, lane, twh[4], sg[5]);
     const c2 ow = cmv(A1, w128);
     const c2 X0 = A0 + ow, X1 = A0 - ow;         // bins r0, r1 of chirp k
-    tile0[k2] = X0;
-    s_t1[k * 64 + lane] = X1;
-    pm0 = fmaxf(pm0, abs2v(X0));
-    pm1 = fmaxf(pm1, abs2v(X1));
-    ms0 += X0;
-    ms1 += X1;
+    tile0[k2] = tof(X0);
+    L.t1[k * 64 + lane] = X1;
+    if (f == a.probe_frame && k == a.probe_chirp && a.probe_mag) {   // :410-411 |cube(:, col)|
+      a.probe_mag[r0] = sqrtf(abs2v(X0));
+      a.probe_mag[r1] = sqrtf(abs2v(X1));
+    }
   }
 
-  // ---------------- per-row reductions over the 16 waves -------------------
-  __syncthreads();                               // taps no longer read
-  red0[(w * 64 + lane) * 3 + 0] = ms0.x;
-  red0[(w * 64 + lane) * 3 + 1] = ms0.y;
-  red0[(w * 64 + lane) * 3 + 2] = pm0;
-  red1[(w * 64 + lane) * 3 + 0] = ms1.x;
-  red1[(w * 64 + lane) * 3 + 1] = ms1.y;
-  red1[(w * 64 + lane) * 3 + 2] = pm1;
+  // ---------------- per-row reductions over the 8 waves --------------------
+  __syncthreads();                               // slot 1 complete in LDS
+  float2 tile1[CPW];
+#pragma unroll
+  for (int k2 = 0; k2 < CPW; ++k2) tile1[k2] = tof(L.t1[(w + NW * k2) * 64 + lane]);
+  c2 s0 = c2{0.f, 0.f}, s1 = c2{0.f, 0.f};
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int k2 = 0; k2 < CPW; ++k2) {
+    s0 += tov(tile0[k2]);
+    s1 += tov(tile1[k2]);
+    p0 = fmaxf(p0, cabs2(tile0[k2]));
+    p1 = fmaxf(p1, cabs2(tile1[k2]));
+  }
+  __syncthreads();                               // L.t1 read out: reuse it as reduction scratch
+  float* red = reinterpret_cast<float*>(L.t1);   // [slot][wave][lane][3]
+  red[((0 * NW + w) * 64 + lane) * 3 + 0] = s0.x;
+  red[((0 * NW + w) * 64 + lane) * 3 + 1] = s0.y;
+  red[((0 * NW + w) * 64 + lane) * 3 + 2] = p0;
+  red[((1 * NW + w) * 64 + lane) * 3 + 0] = s1.x;
+  red[((1 * NW + w) * 64 + lane) * 3 + 1] = s1.y;
+  red[((1 * NW + w) * 64 + lane) * 3 + 2] = p1;
   __syncthreads();
   if (tid < 128) {
     const int sl = tid >> 6;
-    const float* rr = sl ? red1 : red0;
     c2 sum = c2{0.f, 0.f};
     float pm = 0.f;
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
-      sum += c2{rr[(i * 64 + lane) * 3], rr[(i * 64 + lane) * 3 + 1]};
-      pm = fmaxf(pm, rr[(i * 64 + lane) * 3 + 2]);
+      const float* rr = red + ((sl * NW + i) * 64 + lane) * 3;
+      sum += c2{rr[0], rr[1]};
+      pm = fmaxf(pm, rr[2]);
     }
     const float pr = sqrtf(pm);                                    // :210 / :265 abs(max(X,[],2))
-    s_mu[sl][lane] = sum * (1.0f / (float)C);                      // :217 mean over all chirps
-    s_prof[sl][lane] = pr;
+    L.mu[sl][lane] = sum * (1.0f / (float)C);                      // :217 mean over all chirps
+    L.prof[sl][lane] = pr;
     a.profile[f * NR + (sl ? r1 : r0)] = pr;
   }
   __syncthreads();
 
-  // ---------------- slow-time candidates (:257-259) and probe (:410-411) ---
+  // ---------------- slow-time candidates (:257-259) -------------------------
   if (w == 0) {
     const double dpb = a.dist_per_bin, lo = a.min_d, hi = a.max_d;
     auto key = [&](int r, float p) {
       const double rng = (double)r * dpb;
       return (r >= 1 && r <= NR - 2 && rng >= lo && rng <= hi && p > a.range_thr) ? p : -1.f;
     };
-    float v0 = key(r0, s_prof[0][lane]), v1 = key(r1, s_prof[1][lane]);
+    float v0 = key(r0, L.prof[0][lane]), v1 = key(r1, L.prof[1][lane]);
 #pragma unroll
     for (int c = 0; c < OP_CAND; ++c) {
       float bv = v0;
@@ -296,7 +360,7 @@ __global__ __launch_bounds__(1024, 1) void k_rd1p(OnePassArgs a) {
       const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
       if (lane == 0) {
         a.cand_idx[(f * OP_TILES + t) * OP_CAND + c] = sel;
-        s_cand[c] = sel;
+        L.cand[c] = sel;
       }
       if (r0 == sel) v0 = -1.f;
       if (r1 == sel) v1 = -1.f;
@@ -305,79 +369,70 @@ __global__ __launch_bounds__(1024, 1) void k_rd1p(OnePassArgs a) {
   __syncthreads();
 #pragma unroll
   for (int c = 0; c < OP_CAND; ++c) {
-    const int rc = s_cand[c];
+    const int rc = L.cand[c];
     if (rc >= 0) {
       const int q = (rc - t) >> 3, sc = q >> 6, lc = bitrev6(q & 63);
       if (lane == lc) {
         float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
 #pragma unroll
-        for (int k2 = 0; k2 < CPW; ++k2)
-          row[w + NW * k2] = sqrtf(abs2v(sc ? s_t1[(w + NW * k2) * 64 + lc] : tile0[k2]));
+        for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = sqrtf(cabs2(sc ? tile1[k2] : tile0[k2]));
       }
     }
   }
-  if (f == a.probe_frame && a.probe_mag && w == (a.probe_chirp % NW)) {
-    const int kp = a.probe_chirp / NW;
-#pragma unroll
-    for (int k2 = 0; k2 < CPW; ++k2)
-      if (k2 == kp) a.probe_mag[r0] = sqrtf(abs2v(tile0[k2]));
-    a.probe_mag[r1] = sqrtf(abs2v(s_t1[a.probe_chirp * 64 + lane]));
-  }
+
   // ---------------- Doppler: :217-219 on every row of the tile -------------
-  // Per slot: each lane's 16-point DFT over its own chirps k2 (W16^(k2 d2)),
-  // twiddle W256^(w d2), corner turn through LDS, 16-point DFT over the
-  // waves (W16^(w d1)); d = d2 + 16 d1.  Slot 0 is transformed before slot 1
-  // is read back from LDS, so at most two 16-value sets are live.
-  float wdk[CPW];
+  // k = w + 8 k2, d = d2 + 32 d1: each lane's 32-point DFT over its own chirps
+  // (W32^(k2 d2)), corner turn through LDS, twiddle W256^(w d2) by the reader,
+  // 8-point DFT over the waves (W8^(w d1)).
+  auto pre = [&](float2 (&x)[CPW], c2 mu) {
 #pragma unroll
-  for (int k2 = 0; k2 < CPW; ++k2) wdk[k2] = a.wd[w + NW * k2];
-  const int lb = tid / CPW, d2o = tid % CPW;     // corner-turn reader: row lane lb, column d2o
-  const int rb0 = t + 8 * bitrev6(lb);
-  auto pre = [&](c2 (&x)[CPW], c2 mu, float2 (&z)[CPW]) {
-#pragma unroll
-    for (int k2 = 0; k2 < CPW; ++k2) z[k2] = tof((x[k2] - mu) * wdk[k2]);   // :218 (X - mean) .* 2chebwin
-    dft<CPW>(z);
-#pragma unroll
-    for (int d2 = 1; d2 < CPW; ++d2) z[d2] = cmul(z[d2], a.tw_nd[(w * d2) & (ND - 1)]);
+    for (int k2 = 0; k2 < CPW; ++k2) x[k2] = tof((tov(x[k2]) - mu) * sload(a.wd, w + NW * k2));   // :218 (X - mean) .* 2chebwin
+    dft32(x);
   };
-  auto post = [&](float2 (&z)[CPW], int sl) {
+  c2* stg = L.t1;                                // [wave][row lane][d2 ^ (lane & 31)]: conflict-free both ways
+  auto post = [&](const float2 (&z)[CPW], int sl) {
 #pragma unroll
-    for (int d2 = 0; d2 < CPW; ++d2) s_stg[(w * 64 + lane) * SROW + d2] = tov(z[d2]);
+    for (int d2 = 0; d2 < CPW; ++d2) stg[(w * 64 + lane) * CPW + (d2 ^ (lane & 31))] = tov(z[d2]);
     __syncthreads();
-    float2 v[NW];
+    const int d2o = tid & 31;
+    float2 tw[NW];                               // W256^(i d2o): the inter-stage twiddle, applied by the reader
 #pragma unroll
-    for (int i = 0; i < NW; ++i) v[i] = tof(s_stg[(i * 64 + lb) * SROW + d2o]);
-    dft<NW>(v);
-    const int r = rb0 + 512 * sl;
-    float2* __restrict__ out = a.rd ? a.rd + (f * NR + r) * (int64_t)ND : nullptr;
-    float bv = -1.f;
-    int bi = INT_MAX;
+    for (int i = 1; i < NW; ++i) tw[i] = a.tw_nd[(i * d2o) & (ND - 1)];
 #pragma unroll
-    for (int d1s = 0; d1s < NW; ++d1s) {                            // :219 fftshift(., 2)
-      const float2 val = v[(d1s + NW / 2) & (NW - 1)];
-      const int e = d2o + CPW * d1s;
-      const float mag = sqrtf(cabs2(val));
-      if (mag > bv) { bv = mag; bi = e; }
-      if (out) out[e] = val;
+    for (int pass = 0; pass < 4; ++pass) {       // 16 rows per pass, 32 threads per row
+      const int lb = (tid >> 5) + 16 * pass;
+      float2 v[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) v[i] = tof(stg[(i * 64 + lb) * CPW + (d2o ^ (lb & 31))]);
+#pragma unroll
+      for (int i = 1; i < NW; ++i) v[i] = cmul(v[i], tw[i]);
+      dft<NW>(v);
+      const int r = t + 8 * bitrev6(lb) + 512 * sl;
+      float2* __restrict__ out = a.rd ? a.rd + (f * NR + r) * (int64_t)ND : nullptr;
+      float bv = -1.f;
+      int bi = INT_MAX;
+#pragma unroll
+      for (int d1s = 0; d1s < NW; ++d1s) {                          // :219 fftshift(., 2)
+        const float2 val = v[(d1s + NW / 2) & (NW - 1)];
+        const int e = d2o + CPW * d1s;
+        const float mag = sqrtf(cabs2(val));
+        if (mag > bv) { bv = mag; bi = e; }
+        if (out) out[e] = val;
+      }
+#pragma unroll
+      for (int o = CPW / 2; o > 0; o >>= 1) {                       // :233 max(abs(.)) over the row
+        const float ov = __shfl_xor(bv, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      if (d2o == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(bv), bi);
     }
-#pragma unroll
-    for (int o = CPW / 2; o > 0; o >>= 1) {                         // :233 max(abs(.)) over the row
-      const float ov = __shfl_xor(bv, o);
-      const int oi = __shfl_xor(bi, o);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    if (d2o == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(bv), bi);
   };
-  float2 z[CPW];
-  pre(tile0, s_mu[0][lane], z);
-  c2 tile1[CPW];
-#pragma unroll
-  for (int k2 = 0; k2 < CPW; ++k2) tile1[k2] = s_t1[(w + NW * k2) * 64 + lane];
-  __syncthreads();                               // slot 1 read out of LDS: the corner turn may overwrite it
-  post(z, 0);
-  pre(tile1, s_mu[1][lane], z);
+  pre(tile0, L.mu[0][lane]);
+  pre(tile1, L.mu[1][lane]);
+  post(tile0, 0);
   __syncthreads();                               // slot-0 corner turn read out
-  post(z, 1);
+  post(tile1, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -475,9 +530,9 @@ hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s) {
   if (!onepass_supported(a.S, a.C, op::NR, a.C)) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)(((a.F + 7) / 8) * 64);
   if (a.S == op::NR)
-    hipLaunchKernelGGL((k_rd1p<16, true>), dim3(blocks), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL((k_rd1p<true>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
   else
-    hipLaunchKernelGGL((k_rd1p<16, false>), dim3(blocks), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL((k_rd1p<false>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
   return hipGetLastError();
 }
 

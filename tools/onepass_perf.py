@@ -1,6 +1,6 @@
 """Device-side timing of the range+Doppler(+detect) path per schedule (development probe).
 
-python tools/onepass_perf.py [F] [reps] -> one line per schedule: ms per F frames, frames/s,
+python tools/onepass_perf.py [F] [reps] [streams,onepass] -> one line per schedule: ms per F frames, frames/s,
 algorithmic TB/s (SURVEY 8d config-3 bytes), and the per-kernel event averages.
 """
 import os
@@ -15,7 +15,7 @@ from fmcw_radar_processing_amd import params as P  # noqa: E402
 from fmcw_radar_processing_amd.engine import Engine  # noqa: E402
 
 
-def main(F=4096, reps=10):
+def main(F=4096, reps=10, which="streams,onepass"):
     cfg = P.config(3)
     e = Engine(0)
     e.set_taps(cfg, P.synth_calibration(cfg.nts))
@@ -32,6 +32,8 @@ def main(F=4096, reps=10):
     d_rd = torch.empty((F, cfg.nr, cfg.nd, 2), dtype=torch.float32, device=dev)
     byt = F * (cfg.pn * cfg.nts * 8 + cfg.nr * cfg.nd * 8 + cfg.nr * 4 + cfg.pn * 4)
     for name, mode in (("streams", FMCW_PIPE_STREAMS), ("onepass", FMCW_PIPE_ONEPASS)):
+        if name not in which.split(","):
+            continue
         e.set_pipeline(mode)
         e.process_device(d_iq, F, FMCW_C64, outs, d_rd=d_rd, stream=s)
         torch.cuda.synchronize()
@@ -56,5 +58,5 @@ def main(F=4096, reps=10):
 
 
 if __name__ == "__main__":
-    a = [int(x) for x in sys.argv[1:]]
-    main(*a)
+    a = sys.argv[1:]
+    main(*[int(x) for x in a[:2]], *a[2:3])

@@ -29,7 +29,7 @@ def load_counters(path):
     return per, dur
 
 
-LABELS = ("k_range", "k_doppler", "k_detect", "k_rd_fused", "k_compact", "k_stft_power", "k_stft_db")
+LABELS = ("k_range", "k_doppler", "k_detect_1p", "k_detect", "k_rd1p", "k_slow_fix", "k_rd_fused", "k_compact", "k_stft_power", "k_stft_db")
 
 
 def label(k):
@@ -51,7 +51,7 @@ def main(d, json_out=None, bench_log=None):
                 stat_us[short(r['Name'])] = (float(r['AverageNs']) / 1e3, int(r['Calls']))
                 print(f"{short(r['Name']):72s} {int(r['Calls']):6d} {float(r['AverageNs'])/1e3:9.2f} "
                       f"{float(r['TotalDurationNs'])/1e6:9.2f} {float(r['Percentage']):6.2f}")
-    for sub in ("fetch", "write", "sq", "tcc"):
+    for sub in ("fetch", "write", "sq", "tcc", "sq2"):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -78,6 +78,14 @@ def main(d, json_out=None, bench_log=None):
                              f"active {r.get('SQ_ACTIVE_INST_ANY',0)/wc:.2f} valu {r.get('SQ_ACTIVE_INST_VALU',0)/wc:.2f}")
             if "SQ_LDS_BANK_CONFLICT" in r:
                 parts.append(f"lds_conf {r['SQ_LDS_BANK_CONFLICT']:.0f}")
+            if "SQ_INSTS_VMEM_RD" in r:
+                parts.append("insts " + " ".join(f"{c[9:].lower()}={r[c]:.0f}" for c in
+                             ("SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_FLAT")
+                             if c in r) + f" valu={r.get('SQ_INSTS_VALU', 0):.0f}")
+                wc = r.get("SQ_WAVE_CYCLES", 0)
+                if wc:
+                    parts.append(f"wait_lds {r.get('SQ_WAIT_INST_LDS', 0)/wc:.2f} active_lds {r.get('SQ_ACTIVE_INST_LDS', 0)/wc:.2f} "
+                                 f"vmem_rd_cyc {r.get('SQ_INST_CYCLES_VMEM_RD', 0)/wc:.2f}")
             if "GRBM_GUI_ACTIVE" in r:
                 parts.append(f"gui_active {r['GRBM_GUI_ACTIVE']:.0f}")
             print(f"{k:72s} " + " | ".join(parts))
