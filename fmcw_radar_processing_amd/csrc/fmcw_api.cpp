@@ -95,6 +95,8 @@ struct fmcw_ctx {
   int pipe_mode = FMCW_PIPE_AUTO, pipe_nslot = 2;
   DevBuf fused_ctrl, fused_slots, fused_rd_slots, fused_sticky;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
+  DevBuf op_gh;                                // single-pass: {Gh, Hh} per range bin
+  float op_gh_scale = 0.f;                     // IF_scale op_gh was built for (0 = stale)
   bool fused_ran = false;
   int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
   struct Pending {
@@ -314,6 +316,7 @@ int fmcw_set_taps(fmcw_ctx* c, const fmcw_params* p, const float* range_win, con
   CHK(upload_twiddles(c->tw_nd, p->nd, s));
   c->p = *p;
   c->taps = true;
+  c->op_gh_scale = 0.f;
   return FMCW_OK;
 }
 
@@ -446,6 +449,45 @@ static int process_fused(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, in
   return FMCW_OK;
 }
 
+// Per-bin linearity constants of the single-pass range stage (kernels_onepass.hip):
+// Gh[r] = DFT((cal - mean(cal)) w')[r], Hh[r] = DFT(w')[r], w' = float(IF_scale w)
+// (the values K1 uses), accumulated in float64 and rounded once.
+static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
+  const int S = c->p.nts, NR = c->p.nr, n = std::min(S, NR);
+  std::vector<double> cr(NR), ci(NR);
+  for (int i = 0; i < NR; ++i) {
+    const double a = -2.0 * M_PI * (double)i / (double)NR;
+    cr[i] = std::cos(a);
+    ci[i] = std::sin(a);
+  }
+  double mr = 0, mi = 0;
+  for (int i = 0; i < S; ++i) { mr += c->h_cal[2 * i]; mi += c->h_cal[2 * i + 1]; }
+  mr /= S;
+  mi /= S;
+  std::vector<double> wf(n), gr(n), gi(n);
+  for (int i = 0; i < n; ++i) {
+    wf[i] = (double)(float)((double)if_scale * c->h_wr[i]);
+    gr[i] = ((double)c->h_cal[2 * i] - mr) * wf[i];
+    gi[i] = ((double)c->h_cal[2 * i + 1] - mi) * wf[i];
+  }
+  std::vector<float> t(4 * (size_t)NR);
+  for (int r = 0; r < NR; ++r) {
+    double Gr = 0, Gi = 0, Hr = 0, Hi = 0;
+    for (int i = 0, idx = 0; i < n; ++i, idx = (idx + r) & (NR - 1)) {
+      Gr += gr[i] * cr[idx] - gi[i] * ci[idx];
+      Gi += gr[i] * ci[idx] + gi[i] * cr[idx];
+      Hr += wf[i] * cr[idx];
+      Hi += wf[i] * ci[idx];
+    }
+    t[4 * r] = (float)Gr; t[4 * r + 1] = (float)Gi; t[4 * r + 2] = (float)Hr; t[4 * r + 3] = (float)Hi;
+  }
+  CHK(c->op_gh.ensure(t.size() * 4));
+  HIPCHK(hipMemcpyAsync(c->op_gh.p, t.data(), t.size() * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  c->op_gh_scale = if_scale;
+  return FMCW_OK;
+}
+
 // Single-pass schedule (kernels_onepass.hip): k_rd1p computes range FFT,
 // profile, Doppler FFT and the per-row Doppler peaks of each frame without a
 // range cube; k_detect_1p runs the detection; k_slow_fix recomputes the rare
@@ -465,6 +507,14 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   int32_t* fix_list = fix_count + 4;
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
   const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
+  if (c->op_gh_scale != p->if_scale || !c->op_gh.p) CHK(build_onepass_gh(c, p->if_scale, s));
+  if (pframe >= 0 && d_probe) {                // :410-411 fft_data column: one chirp by a direct DFT
+    fmcw::ProbeArgs pa{};
+    pa.iq = static_cast<const float2*>(d_iq);
+    pa.frame = pframe; pa.chirp = pchirp; pa.C = C; pa.S = S; pa.NR = NR;
+    pa.calw = c->calw.as<float4>(); pa.tw_nr = c->tw_nr.as<float2>(); pa.probe_mag = d_probe;
+    HIPCHK(fmcw::launch_probe(pa, s));
+  }
   StageTimer span(c, 7, s, 1);
   for (int64_t f0 = 0; f0 < F; f0 += chunk) {
     const int64_t nf = std::min(chunk, F - f0);
@@ -472,7 +522,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.iq = static_cast<const float2*>(d_iq) + (size_t)f0 * C * S;
     a.F = nf; a.C = C; a.S = S;
     a.calw = c->calw.as<float4>();
-    a.cal_mean = make_float2(c->cal_sum.x / S, c->cal_sum.y / S);
+    a.gh = c->op_gh.as<float4>();
     a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
     a.rd = d_rd ? static_cast<float2*>(d_rd) + (size_t)f0 * NR * ND : nullptr;
     a.profile = d_prof + f0 * NR;
@@ -480,9 +530,6 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.cand_idx = c->op_cidx.as<int32_t>();
     a.cand_rows = c->op_crows.as<float>();
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
-    a.probe_frame = (pframe >= f0 && pframe < f0 + nf) ? pframe - f0 : -1;
-    a.probe_chirp = pchirp;
-    a.probe_mag = d_probe;
     {
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;

@@ -109,7 +109,7 @@ struct OnePassArgs {
   int64_t F;
   int C, S;                // NR = 1024, ND = C (kernel template)
   const float4* calw;      // [S] {cal.re, cal.im, IF_scale*w, w}
-  float2 cal_mean;         // mean(cal) over the S samples (linearity form of :203-204)
+  const float4* gh;        // [NR] {Gh, Hh}: DFT((cal - mean(cal)) w') and DFT(w') per bin (host, float64)
   const float2* tw_nr;     // [NR]
   const float2* tw_nd;     // [ND]
   const float* wd;         // [C]
@@ -119,9 +119,6 @@ struct OnePassArgs {
   int32_t* cand_idx;       // [F][OP_TILES][OP_CAND] 0-based bin or -1
   float* cand_rows;        // [F][OP_TILES][OP_CAND][C] |X[bin, k]|
   float range_thr, min_d, max_d, dist_per_bin;
-  int64_t probe_frame;     // frame within this launch, -1 = none
-  int probe_chirp;
-  float* probe_mag;        // [NR]
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
 };
@@ -157,6 +154,16 @@ struct SlowFixArgs {
 hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s);
 hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s);
 hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s);
+
+struct ProbeArgs {          // fft_data column (:410-411) for the single-pass schedule
+  const float2* iq;        // [F][C][S] of the launch
+  int64_t frame;
+  int chirp, C, S, NR;
+  const float4* calw;
+  const float2* tw_nr;
+  float* probe_mag;        // [NR]
+};
+hipError_t launch_probe(const ProbeArgs& a, hipStream_t s);
 bool onepass_supported(int nts, int pn, int nr, int nd);
 
 struct StftArgs {

@@ -9,43 +9,49 @@
 // partial range FFT cheap:
 //
 //   n = a + 128 b (a < 128, b < 8),  r = t + 8 m (m < 128):
-//   X[t + 8m] = sum_a W128^(a m) * [ W1024^(a t) * sum_b y[a + 128 b] W8^(b t) ]
+//   X[t + 8m] = sum_a W128^(a m) * [ sum_b y[a + 128 b] W1024^(t (a + 128 b)) ]
 //
 // i.e. an in-lane 8-term sum ("stage A") and one 128-point FFT per chirp.  The
 // price is that each of the 8 tiles reads the whole frame: 1 read from HBM and
 // 7 from the XCD's L2.  Blocks b and b+8 share an XCD, so the 8 tiles of a
 // frame are blocks 64j + 8t + x (same x): dispatched together, same L2.
 //
-// Calibration and mean removal (:203-204) enter by linearity.  With
-// y[n] = (x[n] - cal[n] - mu) w'[n] (w' = IF_scale * 2 blackman, :205) and
-// mu = mean(x) - mean(cal):
-//   stage A = sum_b x w' W8^(bt) - G_t[a] - mean(x) H_t[a],
-//   G_t[a] = sum_b (cal - mean(cal)) w' W8^(bt),  H_t[a] = sum_b w' W8^(bt),
-// two per-lane constants per sub-sequence (built once per workgroup, in LDS),
-// so a chirp is consumed straight from its loads: no calibrated copy, and the
-// chirp mean is one wave sum that is applied after stage A.
+// The kernel is VALU-issue bound, so the arithmetic is arranged for the fewest
+// wave instructions:
+// - Calibration and mean removal (:203-204) enter by linearity.  With
+//   y[n] = (x[n] - cal[n] - mu) w'[n] (w' = IF_scale * 2 blackman, :205) and
+//   mu = mean(x) - mean(cal):
+//     X[r] = sum_n x[n] c_t[n] W128^(a m)... - Gh[r] - mean(x) Hh[r],
+//     Gh[r] = DFT((cal - mean(cal)) w')[r],  Hh[r] = DFT(w')[r],
+//   where c_t[n] = w'[n] W1024^(t n) are 16 per-lane constants and Gh/Hh a
+//   per-bin table built on the host in float64 (fmcw_api.cpp).  Stage A is 16
+//   complex MACs straight from the loads, and the chirp mean (one wave sum) is
+//   applied after the FFT.
+// - Complex MACs against per-lane constants are two v_pk_fma_f32 with op_sel /
+//   neg_lo modifiers (inline asm: the compiler would keep a rotated copy of
+//   every constant), wave sums use DPP-fused adds, the Doppler DFTs run on
+//   packed pairs, and the Doppler peak search compares squared magnitudes.
 //
 // Per chirp (one wave, 16 samples per lane as 8 float4 loads, lane l holds
-// a = 2l and 2l+1): stage A as the float4s arrive (the next chirp's first half
-// is requested as soon as this chirp's first half is consumed: a rolling
-// prefetch that keeps >= 4 loads per lane in flight in 32 VGPRs), the mean
-// correction, a 64-point cross-lane DIF FFT on each of the two sub-sequences
-// (DPP and v_permlane16/32_swap exchanges, no LDS), one in-lane radix-2 ->
-// bins r(l, s) = t + 8 (bitrev6(l) + 64 s), s = 0, 1.
-// Wave w handles chirps k = w + 16 k2 (k2 < 16): slot 0 in VGPRs, slot 1 in LDS.
+// a = 2l and 2l+1): stage A, a 64-point cross-lane DIF FFT on each of the two
+// sub-sequences (DPP and v_permlane16/32_swap exchanges, no LDS), one in-lane
+// radix-2 -> bins r(l, s) = t + 8 (bitrev6(l) + 64 s), s = 0, 1, then the
+// Gh/Hh correction.  Loads run two chirps ahead (a 3-deep register ring).
+// Wave w handles chirps k = w + 8 k2 (k2 < 32): slot 0 in VGPRs, slot 1 in LDS.
 //
 // Doppler (:216-219) for every row of the tile: the mean over chirps and the
 // max-abs profile (:210, :265) are reduced across waves in LDS; each lane runs
-// a 16-point DFT over its own chirps (k2), twiddles by W256^(w d2), and the
-// last 16-point DFT over the waves goes through an XOR-swizzled LDS corner
-// turn (the slot-1 region, 128 KiB), one slot (64 rows) at a time; fftshift
-// is folded into the store index.  Each row's max |D| and its first argmax
-// (:233) are kept so detection never reads RD.
+// a 32-point DFT over its own chirps (k2), a swizzled LDS corner turn (the
+// slot-1 region, 128 KiB) hands each (row, d2) column to one thread, which
+// applies W256^(w d2) and the 8-point DFT over the waves; fftshift is folded
+// into the store index.  Each row's max |D| and its first argmax (:233) are
+// kept so detection never reads RD.
 //
 // Slow-time row (:257-259): the target bin is only known once all 8 tiles'
 // profiles exist, so each tile stores |X[r, :]| for its OP_CAND strongest
 // in-window bins above range_threshold; k_detect_1p copies the selected row
 // from there, and k_slow_fix recomputes the rare row that is not a candidate.
+// The fft_data probe (:410-411) is k_probe, a direct DFT of the one chirp.
 #include "frame_ops.h"
 #include "../../include/fmcw.h"
 
@@ -64,21 +70,42 @@ __device__ __forceinline__ c2 cmv(c2 a, c2 b) { return __builtin_elementwise_fma
 __device__ __forceinline__ c2 cmacv(c2 acc, c2 a, c2 b, c2 bs) {
   return __builtin_elementwise_fma(a.yy, bs, __builtin_elementwise_fma(a.xx, b, acc));
 }
+// acc + a * b and a * b against a per-lane VGPR constant b: the rotation of b
+// is done by operand modifiers (op_sel picks b.im for the low half, neg_lo
+// negates it), so no rotated copy of b is kept.  Results must not feed a
+// DPP / permlane op directly (the hazard recognizer does not see inline asm).
+__device__ __forceinline__ c2 cmac_a(c2 acc, c2 a, c2 b) {
+  c2 t, r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(a), "v"(b), "v"(acc));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
+__device__ __forceinline__ c2 cmul_a(c2 a, c2 b) {
+  c2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
+  return r;
+}
 __device__ __forceinline__ c2 tov(float2 v) { return c2{v.x, v.y}; }
 __device__ __forceinline__ float2 tof(c2 v) { return make_float2(v.x, v.y); }
 __device__ __forceinline__ float abs2v(c2 v) { return fmaf(v.x, v.x, v.y * v.y); }
+__device__ __forceinline__ c2 mnegi(c2 a) { return c2{a.y, -a.x}; }   // a * (-i)
 
+// DPP lane read; old = 0 with bound_ctrl lets the compiler fuse the move
+// into the consuming VOP2 (v_add_f32_dpp, v_max_u32_dpp, ...).
 template <int CTRL> __device__ __forceinline__ float dppf(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+template <int CTRL> __device__ __forceinline__ int dppi(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
 }
 
 // Value of lane ^ H, H < 16, by DPP (FFT data: not uniform inside groups).
-template <int H> __device__ __forceinline__ float xpart(float v, int lane) {
+template <int H> __device__ __forceinline__ float xpart(float v) {
   if constexpr (H == 1) return dppf<0xB1>(v);            // quad_perm [1,0,3,2]
   if constexpr (H == 2) return dppf<0x4E>(v);            // quad_perm [2,3,0,1]
   if constexpr (H == 8) return dppf<0x128>(v);           // row_ror:8 == xor 8 inside a row
-  const float p = dppf<0x12C>(v), m = dppf<0x124>(v);    // row_ror:12 (l+4), row_ror:4 (l-4)
-  return (lane & 4) ? m : p;
+  return dppf<0x1B>(dppf<0x141>(v));                     // row_half_mirror (7-i), then quad_perm [3,2,1,0]: i ^ 4
 }
 // (value of the bit-H-clear lane, value of the bit-H-set lane) of this lane's pair, H = 16, 32
 template <int H> __device__ __forceinline__ void xhalves(float v, float& lo, float& hi) {
@@ -111,7 +138,7 @@ __device__ __forceinline__ float wave_sum(float v) {
 // One radix-2 DIF stage of span H across lanes: bit-H-clear lane -> a + b,
 // bit-H-set lane -> (a - b) * tw.  sg = -1 on set lanes, +1 on clear lanes.
 template <int H>
-__device__ __forceinline__ c2 dif_stage(c2 x, int lane, c2 tw, float sg) {
+__device__ __forceinline__ c2 dif_stage(c2 x, c2 tw, float sg) {
   c2 u;
   if constexpr (H >= 16) {
     float lr, hr, li, hi;
@@ -119,7 +146,7 @@ __device__ __forceinline__ c2 dif_stage(c2 x, int lane, c2 tw, float sg) {
     xhalves<H>(x.y, li, hi);
     u = __builtin_elementwise_fma(c2{sg, sg}, c2{hr, hi}, c2{lr, li});
   } else {
-    const c2 o = c2{xpart<H>(x.x, lane), xpart<H>(x.y, lane)};   // the partner's value
+    const c2 o = c2{xpart<H>(x.x), xpart<H>(x.y)};               // the partner's value
     u = __builtin_elementwise_fma(c2{sg, sg}, x, o);              // clear: o + x, set: o - x
   }
   return H == 1 ? u : cmv(u, tw);
@@ -137,9 +164,57 @@ __device__ __forceinline__ float2 sload(const float2* p, int i) {
 
 __device__ __forceinline__ int bitrev6(int l) { return (int)(__brev((unsigned)l) >> 26); }
 
-
-// 32-point forward DFT in registers (natural order): radix-2 over two dft<16>.
-__device__ __forceinline__ void dft32(float2 (&v)[32]) {
+// ---- packed small DFTs (natural order in and out) ------------------------
+__device__ __forceinline__ void dft4p(c2& a0, c2& a1, c2& a2, c2& a3) {
+  const c2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = mnegi(a1 - a3);
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = t1 + t3;
+  a3 = t1 - t3;
+}
+constexpr float kH = 0.70710678118654752440f;
+__device__ __forceinline__ void dft8p(c2 (&v)[8]) {
+  c2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  c2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+  dft4p(e0, e1, e2, e3);
+  dft4p(o0, o1, o2, o3);
+  o1 = c2{o1.x + o1.y, o1.y - o1.x} * kH;       // * W8^1 = h(1 - i)
+  o2 = mnegi(o2);                                // * W8^2 = -i
+  o3 = c2{o3.y - o3.x, -(o3.x + o3.y)} * kH;    // * W8^3 = h(-1 - i)
+  v[0] = e0 + o0; v[4] = e0 - o0;
+  v[1] = e1 + o1; v[5] = e1 - o1;
+  v[2] = e2 + o2; v[6] = e2 - o2;
+  v[3] = e3 + o3; v[7] = e3 - o3;
+}
+// 16 points: X[k1 + 4 k2] = sum_n2 W4^(n2 k2) W16^(n2 k1) sum_n1 x[4 n1 + n2] W4^(n1 k1)
+template <int STRIDE>
+__device__ __forceinline__ void dft16p(c2* v) {
+  c2 y[16];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; ++n2) {
+    c2 a0 = v[STRIDE * n2], a1 = v[STRIDE * (4 + n2)], a2 = v[STRIDE * (8 + n2)], a3 = v[STRIDE * (12 + n2)];
+    dft4p(a0, a1, a2, a3);
+    y[4 * n2 + 0] = a0; y[4 * n2 + 1] = a1; y[4 * n2 + 2] = a2; y[4 * n2 + 3] = a3;
+  }
+  constexpr float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+  y[5] = cmv(y[5], c2{c1, -s1});
+  y[6] = cmv(y[6], c2{kH, -kH});
+  y[7] = cmv(y[7], c2{s1, -c1});
+  y[9] = cmv(y[9], c2{kH, -kH});
+  y[10] = mnegi(y[10]);
+  y[11] = cmv(y[11], c2{-kH, -kH});
+  y[13] = cmv(y[13], c2{s1, -c1});
+  y[14] = cmv(y[14], c2{-kH, -kH});
+  y[15] = cmv(y[15], c2{-c1, s1});
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    c2 a0 = y[k1], a1 = y[4 + k1], a2 = y[8 + k1], a3 = y[12 + k1];
+    dft4p(a0, a1, a2, a3);
+    v[STRIDE * k1] = a0; v[STRIDE * (k1 + 4)] = a1; v[STRIDE * (k1 + 8)] = a2; v[STRIDE * (k1 + 12)] = a3;
+  }
+}
+// 32 points, in place: radix-2 DIT over the even / odd dft16p (stride 2).
+__device__ __forceinline__ void dft32p(c2 (&v)[32]) {
   constexpr float kc[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
                             0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
                             0.19509032201612826785f, 0.0f, -0.19509032201612826785f, -0.38268343236508977173f,
@@ -150,27 +225,24 @@ __device__ __forceinline__ void dft32(float2 (&v)[32]) {
                             0.98078528040323044913f, 1.0f, 0.98078528040323044913f, 0.92387953251128675613f,
                             0.83146961230254523708f, 0.70710678118654752440f, 0.55557023301960222474f,
                             0.38268343236508977173f, 0.19509032201612826785f};
-  float2 e[16], o[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    e[i] = v[2 * i];
-    o[i] = v[2 * i + 1];
-  }
-  dft<16>(e);
-  dft<16>(o);
+  dft16p<2>(v);                                  // evens: v[2k] = E[k]
+  dft16p<2>(v + 1);                              // odds:  v[2k+1] = O[k]
+  c2 r[32];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    const float2 ot = k == 0 ? o[0] : cmul(o[k], make_float2(kc[k], -ks[k]));   // W32^k
-    v[k] = cadd(e[k], ot);
-    v[k + 16] = csub(e[k], ot);
+    const c2 e = v[2 * k];
+    const c2 ot = k == 0 ? v[1] : (k == 8 ? mnegi(v[17]) : cmv(v[2 * k + 1], c2{kc[k], -ks[k]}));   // W32^k O[k]
+    r[k] = e + ot;
+    r[k + 16] = e - ot;
   }
+#pragma unroll
+  for (int k = 0; k < 32; ++k) v[k] = r[k];
 }
 
 // LDS image of k_rd1p.
 struct Lds1p {
   c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the reduction scratch; then the corner turn
-  c2 w[8 * 64];            // {w'[2l + 128j], w'[2l + 1 + 128j]} at [j][l]
-  c2 g[128], h[128];       // G'_t[a], H'_t[a] (times W1024^(a t))
+  f4v gh[128];             // {Gh, Hh} of bin t + 8 m at [m]
   c2 mu[2][64];
   float prof[2][64];
   int cand[OP_CAND];
@@ -196,38 +268,20 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   if (f >= a.F) return;                          // block-uniform
   const int S = FULL ? NR : a.S;
 
-  // ---- per-workgroup tables: window pairs, G'/H' (linearity constants) ----
-  {
-    const int n0 = 2 * lane + 128 * w;           // (j, l) = (w, lane)
-    L.w[tid] = c2{n0 < S ? a.calw[n0].z : 0.f, n0 + 1 < S ? a.calw[n0 + 1].z : 0.f};
-  }
-  if (tid < 128) {                               // a = tid
-    c2 g = c2{0.f, 0.f}, h = c2{0.f, 0.f};
+  if (tid < 128) L.gh[tid] = reinterpret_cast<const f4v*>(a.gh)[t + 8 * tid];
+  // stage-A constants c_t[n] = w'[n] W1024^(t n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
+  c2 cst[16];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = tid + 128 * j;
-      if (n < S) {
-        const float4 cw = a.calw[n];
-        const c2 c8 = tov(sload(a.tw_nr, (128 * j * t) & (NR - 1)));
-        const c2 cc = c2{cw.x - a.cal_mean.x, cw.y - a.cal_mean.y} * cw.z;
-        g = cmacv(g, cc, c8, c2{-c8.y, c8.x});
-        h = __builtin_elementwise_fma(c2{cw.z, cw.z}, c8, h);
-      }
+  for (int j = 0; j < 8; ++j)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * lane + e + 128 * j;
+      const float wv = n < S ? a.calw[n].z : 0.f;
+      cst[2 * j + e] = tov(a.tw_nr[(t * n) & (NR - 1)]) * wv;
     }
-    const c2 ta = tov(a.tw_nr[(tid * t) & (NR - 1)]);
-    L.g[tid] = cmv(g, ta);
-    L.h[tid] = cmv(h, ta);
-  }
-
-  // per-lane / per-tile twiddles (all from the float64-rounded table)
-  const c2 twa0 = tov(a.tw_nr[(2 * lane * t) & (NR - 1)]);
-  const c2 twa1 = tov(a.tw_nr[((2 * lane + 1) * t) & (NR - 1)]);
-  c2 w8[8], w8s[8];                              // W8^(j t): wave-uniform (SGPRs)
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    w8[j] = tov(sload(a.tw_nr, (128 * j * t) & (NR - 1)));
-    w8s[j] = c2{-w8[j].y, w8[j].x};
-  }
+  c2 cs7[2];                                     // rotated copies for the last, compiler-visible MAC
+  cs7[0] = c2{-cst[14].y, cst[14].x};
+  cs7[1] = c2{-cst[15].y, cst[15].x};
   c2 twh[5];                                     // spans 32, 16, 8, 4, 2 (1 on clear lanes)
   float sg[6];                                   // spans 32 .. 1
 #pragma unroll
@@ -244,7 +298,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   // ---------------- range phase: :203-205 for chirps w + 8 k2 --------------
   const f4v* __restrict__ fr = reinterpret_cast<const f4v*>(a.iq + f * (int64_t)C * S);
   const int S2 = S >> 1;                         // float4 (sample pairs) per chirp
-  const float invS = 1.0f / (float)S;
+  const float ninvS = -1.0f / (float)S;
   auto ld_chirp = [&](int k, f4v (&x)[8]) {
     const f4v* __restrict__ q = fr + (int64_t)k * S2;
 #pragma unroll
@@ -254,7 +308,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       else x[j] = q[p < S2 ? p : 0];
     }
   };
-  float2 tile0[CPW];                             // slot 1 goes to LDS (L.t1)
+  c2 tile0[CPW];                                 // slot 1 goes to LDS (L.t1)
   f4v buf[3][8];                                 // chirp ring: 2 chirps in flight while one is consumed
   ld_chirp(w, buf[0]);
   ld_chirp(w + NW, buf[1]);
@@ -262,60 +316,55 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   for (int k2 = 0; k2 < CPW; ++k2) {
     const int k = w + NW * k2;
     if (k2 + 2 < CPW) ld_chirp(k + 2 * NW, buf[(k2 + 2) % 3]);
-    const f4v (&x)[8] = buf[k2 % 3];
-    c2 B0, B1, sx = c2{0.f, 0.f};
+    f4v x[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {                // stage A straight from the loads
-      f4v v = x[j];
+    for (int j = 0; j < 8; ++j) {
+      x[j] = buf[k2 % 3][j];
       if constexpr (!FULL)
-        if (!(lane + 64 * j < S2)) v = f4v{0.f, 0.f, 0.f, 0.f};
-      const c2 wv = L.w[j * 64 + lane];
-      const c2 z0 = v.xy * wv.x, z1 = v.zw * wv.y;    // x .* (IF_scale * 2 blackman)
-      sx += v.xy + v.zw;
-      if (j == 0) {
-        B0 = z0;
-        B1 = z1;
-      } else {                                   // sum_b y[a + 128 b] W8^(b t)
-        B0 = cmacv(B0, z0, w8[j], w8s[j]);
-        B1 = cmacv(B1, z1, w8[j], w8s[j]);
-      }
+        if (!(lane + 64 * j < S2)) x[j] = f4v{0.f, 0.f, 0.f, 0.f};
     }
-    // :204 mean over the S samples, applied after stage A (linearity)
-    const c2 mx = c2{wave_sum(sx.x), wave_sum(sx.y)} * invS;
-    const c2 mxs = c2{-mx.y, mx.x};
-    const f4v g = reinterpret_cast<const f4v*>(L.g)[lane];
-    const f4v h = reinterpret_cast<const f4v*>(L.h)[lane];
-    c2 A0 = cmv(B0, twa0) - cmacv(g.xy, h.xy, mx, mxs);   // * W1024^(a t), - G' - mean(x) H'
-    c2 A1 = cmv(B1, twa1) - cmacv(g.zw, h.zw, mx, mxs);
-    A0 = dif_stage<32>(A0, lane, twh[0], sg[0]); A1 = dif_stage<32>(A1, lane, twh[0], sg[0]);
-    A0 = dif_stage<16>(A0, lane, twh[1], sg[1]); A1 = dif_stage<16>(A1, lane, twh[1], sg[1]);
-    A0 = dif_stage<8>(A0, lane, twh[2], sg[2]);  A1 = dif_stage<8>(A1, lane, twh[2], sg[2]);
-    A0 = dif_stage<4>(A0, lane, twh[3], sg[3]);  A1 = dif_stage<4>(A1, lane, twh[3], sg[3]);
-    A0 = dif_stage<2>(A0, lane, twh[4], sg[4]);  A1 = dif_stage<2>(A1, lane, twh[4], sg[4]);
-    A0 = dif_stage<1>(A0, lane, twh[4], sg[5]);  A1 = dif_stage<1>(A1, lane, twh[4], sg[5]);
+    // stage A: sum_b x[a + 128 b] c_t[a + 128 b], straight from the loads
+    c2 A0 = cmul_a(x[0].xy, cst[0]), A1 = cmul_a(x[0].zw, cst[1]);
+    f4v s4 = x[0];
+#pragma unroll
+    for (int j = 1; j < 7; ++j) {
+      A0 = cmac_a(A0, x[j].xy, cst[2 * j]);
+      A1 = cmac_a(A1, x[j].zw, cst[2 * j + 1]);
+      s4 += x[j];
+    }
+    A0 = cmacv(A0, x[7].xy, cst[14], cs7[0]);   // compiler-visible producer for the DPP stages
+    A1 = cmacv(A1, x[7].zw, cst[15], cs7[1]);
+    s4 += x[7];
+    A0 = dif_stage<32>(A0, twh[0], sg[0]); A1 = dif_stage<32>(A1, twh[0], sg[0]);
+    A0 = dif_stage<16>(A0, twh[1], sg[1]); A1 = dif_stage<16>(A1, twh[1], sg[1]);
+    A0 = dif_stage<8>(A0, twh[2], sg[2]);  A1 = dif_stage<8>(A1, twh[2], sg[2]);
+    A0 = dif_stage<4>(A0, twh[3], sg[3]);  A1 = dif_stage<4>(A1, twh[3], sg[3]);
+    A0 = dif_stage<2>(A0, twh[4], sg[4]);  A1 = dif_stage<2>(A1, twh[4], sg[4]);
+    A0 = dif_stage<1>(A0, twh[4], sg[5]);  A1 = dif_stage<1>(A1, twh[4], sg[5]);
+    // :204 the chirp mean, applied to the spectrum: X -= Gh + mean(x) Hh
+    const c2 sx = s4.xy + s4.zw;
+    const c2 nmx = c2{wave_sum(sx.x), wave_sum(sx.y)} * ninvS;
+    const f4v g0 = L.gh[m0], g1 = L.gh[m0 + 64];
     const c2 ow = cmv(A1, w128);
-    const c2 X0 = A0 + ow, X1 = A0 - ow;         // bins r0, r1 of chirp k
-    tile0[k2] = tof(X0);
+    const c2 X0 = cmac_a(A0 + ow - g0.xy, nmx, g0.zw);   // bin r0 of chirp k
+    const c2 X1 = cmac_a(A0 - ow - g1.xy, nmx, g1.zw);   // bin r1
+    tile0[k2] = X0;
     L.t1[k * 64 + lane] = X1;
-    if (f == a.probe_frame && k == a.probe_chirp && a.probe_mag) {   // :410-411 |cube(:, col)|
-      a.probe_mag[r0] = sqrtf(abs2v(X0));
-      a.probe_mag[r1] = sqrtf(abs2v(X1));
-    }
   }
 
   // ---------------- per-row reductions over the 8 waves --------------------
   __syncthreads();                               // slot 1 complete in LDS
-  float2 tile1[CPW];
+  c2 tile1[CPW];
 #pragma unroll
-  for (int k2 = 0; k2 < CPW; ++k2) tile1[k2] = tof(L.t1[(w + NW * k2) * 64 + lane]);
+  for (int k2 = 0; k2 < CPW; ++k2) tile1[k2] = L.t1[(w + NW * k2) * 64 + lane];
   c2 s0 = c2{0.f, 0.f}, s1 = c2{0.f, 0.f};
   float p0 = 0.f, p1 = 0.f;
 #pragma unroll
   for (int k2 = 0; k2 < CPW; ++k2) {
-    s0 += tov(tile0[k2]);
-    s1 += tov(tile1[k2]);
-    p0 = fmaxf(p0, cabs2(tile0[k2]));
-    p1 = fmaxf(p1, cabs2(tile1[k2]));
+    s0 += tile0[k2];
+    s1 += tile1[k2];
+    p0 = fmaxf(p0, abs2v(tile0[k2]));
+    p1 = fmaxf(p1, abs2v(tile1[k2]));
   }
   __syncthreads();                               // L.t1 read out: reuse it as reduction scratch
   float* red = reinterpret_cast<float*>(L.t1);   // [slot][wave][lane][3]
@@ -375,7 +424,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       if (lane == lc) {
         float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
 #pragma unroll
-        for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = sqrtf(cabs2(sc ? tile1[k2] : tile0[k2]));
+        for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = sqrtf(abs2v(sc ? tile1[k2] : tile0[k2]));
       }
     }
   }
@@ -384,48 +433,61 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   // k = w + 8 k2, d = d2 + 32 d1: each lane's 32-point DFT over its own chirps
   // (W32^(k2 d2)), corner turn through LDS, twiddle W256^(w d2) by the reader,
   // 8-point DFT over the waves (W8^(w d1)).
-  auto pre = [&](float2 (&x)[CPW], c2 mu) {
+  auto pre = [&](c2 (&x)[CPW], c2 mu) {
 #pragma unroll
-    for (int k2 = 0; k2 < CPW; ++k2) x[k2] = tof((tov(x[k2]) - mu) * sload(a.wd, w + NW * k2));   // :218 (X - mean) .* 2chebwin
-    dft32(x);
+    for (int k2 = 0; k2 < CPW; ++k2) x[k2] = (x[k2] - mu) * sload(a.wd, w + NW * k2);   // :218 (X - mean) .* 2chebwin
+    dft32p(x);
   };
   c2* stg = L.t1;                                // [wave][row lane][d2 ^ (lane & 31)]: conflict-free both ways
-  auto post = [&](const float2 (&z)[CPW], int sl) {
+  const int d2o = tid & 31;
+  c2 twr[NW];                                    // W256^(i d2o): the inter-stage twiddle, applied by the reader
 #pragma unroll
-    for (int d2 = 0; d2 < CPW; ++d2) stg[(w * 64 + lane) * CPW + (d2 ^ (lane & 31))] = tov(z[d2]);
+  for (int i = 1; i < NW; ++i) twr[i] = tov(a.tw_nd[(i * d2o) & (ND - 1)]);
+  auto post = [&](const c2 (&z)[CPW], int sl) {
+#pragma unroll
+    for (int d2 = 0; d2 < CPW; ++d2) stg[(w * 64 + lane) * CPW + (d2 ^ (lane & 31))] = z[d2];
     __syncthreads();
-    const int d2o = tid & 31;
-    float2 tw[NW];                               // W256^(i d2o): the inter-stage twiddle, applied by the reader
-#pragma unroll
-    for (int i = 1; i < NW; ++i) tw[i] = a.tw_nd[(i * d2o) & (ND - 1)];
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {       // 16 rows per pass, 32 threads per row
       const int lb = (tid >> 5) + 16 * pass;
-      float2 v[NW];
+      c2 v[NW];
 #pragma unroll
-      for (int i = 0; i < NW; ++i) v[i] = tof(stg[(i * 64 + lb) * CPW + (d2o ^ (lb & 31))]);
+      for (int i = 0; i < NW; ++i) v[i] = stg[(i * 64 + lb) * CPW + (d2o ^ (lb & 31))];
 #pragma unroll
-      for (int i = 1; i < NW; ++i) v[i] = cmul(v[i], tw[i]);
-      dft<NW>(v);
+      for (int i = 1; i < NW; ++i) v[i] = cmul_a(v[i], twr[i]);
+      dft8p(v);
       const int r = t + 8 * bitrev6(lb) + 512 * sl;
-      float2* __restrict__ out = a.rd ? a.rd + (f * NR + r) * (int64_t)ND : nullptr;
-      float bv = -1.f;
-      int bi = INT_MAX;
+      f4v* __restrict__ out = a.rd ? reinterpret_cast<f4v*>(a.rd + (f * NR + r) * (int64_t)ND) : nullptr;
+      // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element e = d2o + 32 d1s
+      float q[NW];
 #pragma unroll
-      for (int d1s = 0; d1s < NW; ++d1s) {                          // :219 fftshift(., 2)
-        const float2 val = v[(d1s + NW / 2) & (NW - 1)];
-        const int e = d2o + CPW * d1s;
-        const float mag = sqrtf(cabs2(val));
-        if (mag > bv) { bv = mag; bi = e; }
-        if (out) out[e] = val;
-      }
+      for (int d1s = 0; d1s < NW; ++d1s) q[d1s] = abs2v(v[(d1s + NW / 2) & (NW - 1)]);
+      if (out) {
 #pragma unroll
-      for (int o = CPW / 2; o > 0; o >>= 1) {                       // :233 max(abs(.)) over the row
-        const float ov = __shfl_xor(bv, o);
-        const int oi = __shfl_xor(bi, o);
-        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        for (int d1s = 0; d1s < NW; ++d1s)
+          reinterpret_cast<c2*>(out)[d2o + CPW * d1s] = v[(d1s + NW / 2) & (NW - 1)];
       }
-      if (d2o == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(bv), bi);
+      // :233 [val, di] = max(abs(.)): exact max of |D|^2 over the row, then its first index
+      float m = q[0];
+#pragma unroll
+      for (int d1s = 1; d1s < NW; ++d1s) m = fmaxf(m, q[d1s]);
+      int mi = __float_as_int(m);                                   // non-negative: int order == float order
+      mi = max(mi, dppi<0xB1>(mi));
+      mi = max(mi, dppi<0x4E>(mi));
+      mi = max(mi, __builtin_amdgcn_ds_swizzle(mi, 0x101F));        // xor 4 (bitmode, 32-lane groups)
+      mi = max(mi, __builtin_amdgcn_ds_swizzle(mi, 0x201F));        // xor 8
+      mi = max(mi, __builtin_amdgcn_ds_swizzle(mi, 0x401F));        // xor 16
+      const float rm = __int_as_float(mi);
+      int e = INT_MAX;
+#pragma unroll
+      for (int d1s = NW - 1; d1s >= 0; --d1s)
+        if (q[d1s] == rm) e = d2o + CPW * d1s;
+      e = min(e, dppi<0xB1>(e));
+      e = min(e, dppi<0x4E>(e));
+      e = min(e, __builtin_amdgcn_ds_swizzle(e, 0x101F));
+      e = min(e, __builtin_amdgcn_ds_swizzle(e, 0x201F));
+      e = min(e, __builtin_amdgcn_ds_swizzle(e, 0x401F));
+      if (d2o == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
     }
   };
   pre(tile0, L.mu[0][lane]);
@@ -433,6 +495,39 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   post(tile0, 0);
   __syncthreads();                               // slot-0 corner turn read out
   post(tile1, 1);
+}
+
+// ---------------------------------------------------------------------------
+// k_probe: |X[:, k]| of one chirp (radar_processing.m:410-411, fft_data column)
+// by a direct DFT: only called when a probe column is requested.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_probe(ProbeArgs a) {
+  __shared__ float2 y[1024];
+  __shared__ float2 red[16];
+  const int tid = threadIdx.x, S = a.S, NR = a.NR;
+  const float2* __restrict__ x = a.iq + (a.frame * (int64_t)a.C + a.chirp) * S;
+  float2 d = make_float2(0.f, 0.f);
+  for (int n = tid; n < S; n += 1024) d = cadd(d, make_float2(x[n].x - a.calw[n].x, x[n].y - a.calw[n].y));
+  d = make_float2(op::wave_sum(d.x), op::wave_sum(d.y));
+  if ((tid & 63) == 0) red[tid >> 6] = d;
+  __syncthreads();
+  float2 mu = make_float2(0.f, 0.f);
+  for (int i = 0; i < 16; ++i) mu = cadd(mu, red[i]);
+  mu = cscale(mu, 1.0f / (float)S);
+  for (int n = tid; n < NR; n += 1024) {
+    float2 v = make_float2(0.f, 0.f);
+    if (n < S) {
+      const float4 c = a.calw[n];
+      v = cscale(make_float2(x[n].x - c.x - mu.x, x[n].y - c.y - mu.y), c.z);
+    }
+    y[n] = v;
+  }
+  __syncthreads();
+  for (int r = tid; r < NR; r += 1024) {
+    float2 acc = make_float2(0.f, 0.f);
+    for (int n = 0; n < NR; ++n) acc = cadd(acc, cmul(y[n], a.tw_nr[((int64_t)n * r) & (NR - 1)]));
+    a.probe_mag[r] = sqrtf(cabs2(acc));
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -545,6 +640,12 @@ hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s) {
 
 hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_slow_fix, dim3(64), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_probe(const ProbeArgs& a, hipStream_t s) {
+  if (a.S > a.NR || a.NR != op::NR) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_probe, dim3(1), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 
