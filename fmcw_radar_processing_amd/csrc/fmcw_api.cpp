@@ -541,7 +541,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     }
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
     fmcw::Detect1pArgs k{};
-    k.profile = a.profile; k.rowpk = a.rowpk; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
+    k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
     k.nframes = (int)nf; k.NR = NR; k.C = C; k.M = M;
     k.det.ND = ND; k.det.C = C; k.det.M = M;
     k.det.range_thr = p->range_thr; k.det.doppler_thr = p->doppler_thr;

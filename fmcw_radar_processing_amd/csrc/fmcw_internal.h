@@ -115,7 +115,7 @@ struct OnePassArgs {
   const float* wd;         // [C]
   float2* rd;              // [F][NR][ND] or nullptr (then only the row peaks are kept)
   float* profile;          // [F][NR]
-  int2* rowpk;             // [F][NR] {float bits of max_d |D[r,d]|, first argmax d (fftshift-ed, 0-based)}
+  int2* rowpk;             // [F][NR] {float bits of max_d |D[r,d]|, first argmax d (fftshift-ed, 0-based)}; only when rd is nullptr
   int32_t* cand_idx;       // [F][OP_TILES][OP_CAND] 0-based bin or -1
   float* cand_rows;        // [F][OP_TILES][OP_CAND][C] |X[bin, k]|
   float range_thr, min_d, max_d, dist_per_bin;
@@ -125,7 +125,9 @@ struct OnePassArgs {
 
 struct Detect1pArgs {
   const float* profile;    // [F][NR]
-  const int2* rowpk;       // [F][NR]
+  const int2* rowpk;       // [F][NR] (used when rd is nullptr)
+  const float2* rd;        // [F][NR][ND] or nullptr
+  int ND;
   const int32_t* cand_idx; // [F][OP_TILES][OP_CAND]
   const float* cand_rows;  // [F][OP_TILES][OP_CAND][C]
   int nframes, NR, C, M;

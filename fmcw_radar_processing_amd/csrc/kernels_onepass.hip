@@ -241,11 +241,9 @@ __device__ __forceinline__ void dft32p(c2 (&v)[32]) {
 
 // LDS image of k_rd1p.
 struct Lds1p {
-  c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the reduction scratch; then the corner turn
+  c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the corner turn
   f4v gh[128];             // {Gh, Hh} of bin t + 8 m at [m]
-  c2 mu[2][64];
-  float prof[2][64];
-  int cand[OP_CAND];
+  float red[2][NW][3][64]; // per-wave {sum.re, sum.im, max |X|^2} of each row over the wave's chirps
 };
 
 }  // namespace op
@@ -353,79 +351,67 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   }
 
   // ---------------- per-row reductions over the 8 waves --------------------
-  __syncthreads();                               // slot 1 complete in LDS
+  __syncthreads();                               // B1: slot 1 complete in LDS
   c2 tile1[CPW];
 #pragma unroll
   for (int k2 = 0; k2 < CPW; ++k2) tile1[k2] = L.t1[(w + NW * k2) * 64 + lane];
-  c2 s0 = c2{0.f, 0.f}, s1 = c2{0.f, 0.f};
-  float p0 = 0.f, p1 = 0.f;
+  {
+    c2 s0 = c2{0.f, 0.f}, s1 = c2{0.f, 0.f};
+    float p0 = 0.f, p1 = 0.f;
 #pragma unroll
-  for (int k2 = 0; k2 < CPW; ++k2) {
-    s0 += tile0[k2];
-    s1 += tile1[k2];
-    p0 = fmaxf(p0, abs2v(tile0[k2]));
-    p1 = fmaxf(p1, abs2v(tile1[k2]));
-  }
-  __syncthreads();                               // L.t1 read out: reuse it as reduction scratch
-  float* red = reinterpret_cast<float*>(L.t1);   // [slot][wave][lane][3]
-  red[((0 * NW + w) * 64 + lane) * 3 + 0] = s0.x;
-  red[((0 * NW + w) * 64 + lane) * 3 + 1] = s0.y;
-  red[((0 * NW + w) * 64 + lane) * 3 + 2] = p0;
-  red[((1 * NW + w) * 64 + lane) * 3 + 0] = s1.x;
-  red[((1 * NW + w) * 64 + lane) * 3 + 1] = s1.y;
-  red[((1 * NW + w) * 64 + lane) * 3 + 2] = p1;
-  __syncthreads();
-  if (tid < 128) {
-    const int sl = tid >> 6;
-    c2 sum = c2{0.f, 0.f};
-    float pm = 0.f;
-#pragma unroll
-    for (int i = 0; i < NW; ++i) {
-      const float* rr = red + ((sl * NW + i) * 64 + lane) * 3;
-      sum += c2{rr[0], rr[1]};
-      pm = fmaxf(pm, rr[2]);
+    for (int k2 = 0; k2 < CPW; ++k2) {
+      s0 += tile0[k2];
+      s1 += tile1[k2];
+      p0 = fmaxf(p0, abs2v(tile0[k2]));
+      p1 = fmaxf(p1, abs2v(tile1[k2]));
     }
-    const float pr = sqrtf(pm);                                    // :210 / :265 abs(max(X,[],2))
-    L.mu[sl][lane] = sum * (1.0f / (float)C);                      // :217 mean over all chirps
-    L.prof[sl][lane] = pr;
-    a.profile[f * NR + (sl ? r1 : r0)] = pr;
+    L.red[0][w][0][lane] = s0.x; L.red[0][w][1][lane] = s0.y; L.red[0][w][2][lane] = p0;
+    L.red[1][w][0][lane] = s1.x; L.red[1][w][1][lane] = s1.y; L.red[1][w][2][lane] = p1;
   }
-  __syncthreads();
+  __syncthreads();                               // B2: partials visible; L.t1 read out (free for the corner turn)
+  // every wave reduces the 8 partials of its lane's two rows in the same order
+  // (identical bits in every wave), so no serial section follows
+  c2 mu0 = c2{0.f, 0.f}, mu1 = c2{0.f, 0.f};
+  float q0 = 0.f, q1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    mu0 += c2{L.red[0][i][0][lane], L.red[0][i][1][lane]};
+    mu1 += c2{L.red[1][i][0][lane], L.red[1][i][1][lane]};
+    q0 = fmaxf(q0, L.red[0][i][2][lane]);
+    q1 = fmaxf(q1, L.red[1][i][2][lane]);
+  }
+  mu0 *= 1.0f / (float)C;                        // :217 mean over all chirps
+  mu1 *= 1.0f / (float)C;
+  const float pr0 = sqrtf(q0), pr1 = sqrtf(q1);  // :210 / :265 abs(max(X,[],2))
+  if (w == 0) {
+    a.profile[f * NR + r0] = pr0;
+    a.profile[f * NR + r1] = pr1;
+  }
 
   // ---------------- slow-time candidates (:257-259) -------------------------
-  if (w == 0) {
+  {
     const double dpb = a.dist_per_bin, lo = a.min_d, hi = a.max_d;
     auto key = [&](int r, float p) {
       const double rng = (double)r * dpb;
       return (r >= 1 && r <= NR - 2 && rng >= lo && rng <= hi && p > a.range_thr) ? p : -1.f;
     };
-    float v0 = key(r0, L.prof[0][lane]), v1 = key(r1, L.prof[1][lane]);
+    float v0 = key(r0, pr0), v1 = key(r1, pr1);
 #pragma unroll
     for (int c = 0; c < OP_CAND; ++c) {
       float bv = v0;
       int bi = r0;
       if (v1 > bv) { bv = v1; bi = r1; }                           // r0 < r1: ties keep r0
-      wave_argmax(bv, bi);
+      wave_argmax(bv, bi);                                          // same result in every wave
       const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
-      if (lane == 0) {
-        a.cand_idx[(f * OP_TILES + t) * OP_CAND + c] = sel;
-        L.cand[c] = sel;
+      if (w == 0 && lane == 0) a.cand_idx[(f * OP_TILES + t) * OP_CAND + c] = sel;
+      if (sel >= 0 && (r0 == sel || r1 == sel)) {
+        float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
+        const bool s1 = r1 == sel;
+#pragma unroll
+        for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = sqrtf(abs2v(s1 ? tile1[k2] : tile0[k2]));
       }
       if (r0 == sel) v0 = -1.f;
       if (r1 == sel) v1 = -1.f;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < OP_CAND; ++c) {
-    const int rc = L.cand[c];
-    if (rc >= 0) {
-      const int q = (rc - t) >> 3, sc = q >> 6, lc = bitrev6(q & 63);
-      if (lane == lc) {
-        float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
-#pragma unroll
-        for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = sqrtf(abs2v(sc ? tile1[k2] : tile0[k2]));
-      }
     }
   }
 
@@ -443,10 +429,29 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   c2 twr[NW];                                    // W256^(i d2o): the inter-stage twiddle, applied by the reader
 #pragma unroll
   for (int i = 1; i < NW; ++i) twr[i] = tov(a.tw_nd[(i * d2o) & (ND - 1)]);
-  auto post = [&](const c2 (&z)[CPW], int sl) {
+  // max / min over the 32 lanes of a row (DPP: xor 1, xor 2, then mirrors on
+  // group-uniform values, then the 16-lane row swap)
+  auto row_max = [&](int v) {
+    v = max(v, dppi<0xB1>(v));
+    v = max(v, dppi<0x4E>(v));
+    v = max(v, dppi<0x141>(v));
+    v = max(v, dppi<0x140>(v));
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return max((int)r[0], (int)r[1]);
+  };
+  auto row_min = [&](int v) {
+    v = min(v, dppi<0xB1>(v));
+    v = min(v, dppi<0x4E>(v));
+    v = min(v, dppi<0x141>(v));
+    v = min(v, dppi<0x140>(v));
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return min((int)r[0], (int)r[1]);
+  };
+  auto stage = [&](const c2 (&z)[CPW]) {
 #pragma unroll
     for (int d2 = 0; d2 < CPW; ++d2) stg[(w * 64 + lane) * CPW + (d2 ^ (lane & 31))] = z[d2];
-    __syncthreads();
+  };
+  auto post = [&](int sl) {
 #pragma unroll
     for (int pass = 0; pass < 4; ++pass) {       // 16 rows per pass, 32 threads per row
       const int lb = (tid >> 5) + 16 * pass;
@@ -457,44 +462,38 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       for (int i = 1; i < NW; ++i) v[i] = cmul_a(v[i], twr[i]);
       dft8p(v);
       const int r = t + 8 * bitrev6(lb) + 512 * sl;
-      f4v* __restrict__ out = a.rd ? reinterpret_cast<f4v*>(a.rd + (f * NR + r) * (int64_t)ND) : nullptr;
       // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element e = d2o + 32 d1s
+      if (a.rd) {                                // RD written: k_detect_1p reads the target rows' peaks from it
+        c2* __restrict__ out = reinterpret_cast<c2*>(a.rd + (f * NR + r) * (int64_t)ND);
+#pragma unroll
+        for (int d1s = 0; d1s < NW; ++d1s) out[d2o + CPW * d1s] = v[(d1s + NW / 2) & (NW - 1)];
+        continue;
+      }
+      // :233 [val, di] = max(abs(.)): exact max of |D|^2 over the row, then its first index
       float q[NW];
 #pragma unroll
       for (int d1s = 0; d1s < NW; ++d1s) q[d1s] = abs2v(v[(d1s + NW / 2) & (NW - 1)]);
-      if (out) {
-#pragma unroll
-        for (int d1s = 0; d1s < NW; ++d1s)
-          reinterpret_cast<c2*>(out)[d2o + CPW * d1s] = v[(d1s + NW / 2) & (NW - 1)];
-      }
-      // :233 [val, di] = max(abs(.)): exact max of |D|^2 over the row, then its first index
       float m = q[0];
 #pragma unroll
       for (int d1s = 1; d1s < NW; ++d1s) m = fmaxf(m, q[d1s]);
-      int mi = __float_as_int(m);                                   // non-negative: int order == float order
-      mi = max(mi, dppi<0xB1>(mi));
-      mi = max(mi, dppi<0x4E>(mi));
-      mi = max(mi, __builtin_amdgcn_ds_swizzle(mi, 0x101F));        // xor 4 (bitmode, 32-lane groups)
-      mi = max(mi, __builtin_amdgcn_ds_swizzle(mi, 0x201F));        // xor 8
-      mi = max(mi, __builtin_amdgcn_ds_swizzle(mi, 0x401F));        // xor 16
-      const float rm = __int_as_float(mi);
+      const float rm = __int_as_float(row_max(__float_as_int(m)));   // non-negative: int order == float order
       int e = INT_MAX;
 #pragma unroll
       for (int d1s = NW - 1; d1s >= 0; --d1s)
         if (q[d1s] == rm) e = d2o + CPW * d1s;
-      e = min(e, dppi<0xB1>(e));
-      e = min(e, dppi<0x4E>(e));
-      e = min(e, __builtin_amdgcn_ds_swizzle(e, 0x101F));
-      e = min(e, __builtin_amdgcn_ds_swizzle(e, 0x201F));
-      e = min(e, __builtin_amdgcn_ds_swizzle(e, 0x401F));
+      e = row_min(e);
       if (d2o == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
     }
   };
-  pre(tile0, L.mu[0][lane]);
-  pre(tile1, L.mu[1][lane]);
-  post(tile0, 0);
-  __syncthreads();                               // slot-0 corner turn read out
-  post(tile1, 1);
+  pre(tile0, mu0);
+  pre(tile1, mu1);
+  stage(tile0);
+  __syncthreads();                               // B3: slot-0 corner turn written
+  post(0);
+  __syncthreads();                               // B4: slot-0 corner turn read out
+  stage(tile1);
+  __syncthreads();                               // B5
+  post(1);
 }
 
 // ---------------------------------------------------------------------------
@@ -561,13 +560,31 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
   } else {
     for (int k = lane; k < C; k += 64) slow[k] = 0.f;
   }
+  // :233 [val, di] = max(abs(D)) of each target row: from the RD map when it
+  // was written (k_rd1p then skips the per-row peak search), else from rowpk
+  int2 pkr[8];
+  if (a.rd) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < n) {
+        const float2* __restrict__ row = a.rd + (f * NR + sel[j]) * (int64_t)a.ND;
+        float bv = -1.f;
+        int bi = INT_MAX;
+        for (int e = lane; e < a.ND; e += 64) {
+          const float m = sqrtf(cabs2(row[e]));
+          if (m > bv) { bv = m; bi = e; }
+        }
+        wave_argmax(bv, bi);
+        pkr[j] = make_int2(__float_as_int(bv), bi);
+      }
+  }
   if (lane < M) {
     int ri = 0, di = 0;
     float rm = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (j == lane && j < n) {
-        const int2 pk = a.rowpk[f * NR + sel[j]];
+        const int2 pk = a.rd ? pkr[j] : a.rowpk[f * NR + sel[j]];
         di = pk.y + 1;
         if (!(__int_as_float(pk.x) >= q.doppler_thr && di != q.fallback)) di = q.fallback;   // :234-238
         ri = sel[j] + 1;
