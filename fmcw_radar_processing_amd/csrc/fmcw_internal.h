@@ -117,7 +117,7 @@ struct OnePassArgs {
   float* profile;          // [F][NR]
   int2* rowpk;             // [F][NR] {float bits of max_d |D[r,d]|, first argmax d (fftshift-ed, 0-based)}; only when rd is nullptr
   int32_t* cand_idx;       // [F][OP_TILES][OP_CAND] 0-based bin or -1
-  float* cand_rows;        // [F][OP_TILES][OP_CAND][C] |X[bin, k]|
+  float* cand_rows;        // [F][OP_TILES][OP_CAND][C] |X[bin, k]|^2
   float range_thr, min_d, max_d, dist_per_bin;
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
@@ -129,7 +129,7 @@ struct Detect1pArgs {
   const float2* rd;        // [F][NR][ND] or nullptr
   int ND;
   const int32_t* cand_idx; // [F][OP_TILES][OP_CAND]
-  const float* cand_rows;  // [F][OP_TILES][OP_CAND][C]
+  const float* cand_rows;  // [F][OP_TILES][OP_CAND][C] |X|^2
   int nframes, NR, C, M;
   DetectParams det;
   int32_t* count;

@@ -404,11 +404,17 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       wave_argmax(bv, bi);                                          // same result in every wave
       const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
       if (w == 0 && lane == 0) a.cand_idx[(f * OP_TILES + t) * OP_CAND + c] = sel;
-      if (sel >= 0 && (r0 == sel || r1 == sel)) {
-        float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
-        const bool s1 = r1 == sel;
+      // |X[sel, k]|^2 of the candidate row (k_detect_1p takes the square root of
+      // the one row it keeps); the slot is wave-uniform (r1 = r0 + 512)
+      float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
+      if (sel >= 512) {
+        if (r1 == sel)
 #pragma unroll
-        for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = sqrtf(abs2v(s1 ? tile1[k2] : tile0[k2]));
+          for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = abs2v(tile1[k2]);
+      } else if (sel >= 0) {
+        if (r0 == sel)
+#pragma unroll
+          for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = abs2v(tile0[k2]);
       }
       if (r0 == sel) v0 = -1.f;
       if (r1 == sel) v1 = -1.f;
@@ -553,7 +559,7 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
       if (ci[i] == row) c = i;
     if (c >= 0) {
       const float* src = a.cand_rows + ((f * OP_TILES + tt) * OP_CAND + c) * (int64_t)C;
-      for (int k = lane; k < C; k += 64) slow[k] = src[k];
+      for (int k = lane; k < C; k += 64) slow[k] = sqrtf(src[k]);     // candidates hold |X|^2
     } else if (lane == 0) {
       a.fix_list[atomicAdd(a.fix_count, 1)] = (int32_t)f;
     }

@@ -31,9 +31,9 @@ def main(F=4096, reps=10, which="streams,onepass"):
                 slow_mag=torch.empty((F, cfg.pn), device=dev))
     d_rd = torch.empty((F, cfg.nr, cfg.nd, 2), dtype=torch.float32, device=dev)
     byt = F * (cfg.pn * cfg.nts * 8 + cfg.nr * cfg.nd * 8 + cfg.nr * 4 + cfg.pn * 4)
-    for name, mode in (("streams", FMCW_PIPE_STREAMS), ("onepass", FMCW_PIPE_ONEPASS)):
-        if name not in which.split(","):
-            continue
+    modes = {"streams": FMCW_PIPE_STREAMS, "onepass": FMCW_PIPE_ONEPASS}
+    for name in which.split(","):
+        mode = modes[name]
         e.set_pipeline(mode)
         e.process_device(d_iq, F, FMCW_C64, outs, d_rd=d_rd, stream=s)
         torch.cuda.synchronize()
