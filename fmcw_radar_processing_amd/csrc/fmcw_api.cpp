@@ -584,7 +584,9 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   hipStream_t s = pick(c, stream);
   const bool onepass_ok = !d_cube && in_dtype == FMCW_C64 && (!d_rd || out_dtype == FMCW_C64) &&
                           fmcw::onepass_supported(S, C, NR, ND);
-  if (c->pipe_mode == FMCW_PIPE_ONEPASS) {
+  // AUTO = single pass wherever it applies: half the HBM bytes of the streams
+  // schedule (no range cube) and faster on MI355X
+  if (c->pipe_mode == FMCW_PIPE_ONEPASS || (c->pipe_mode == FMCW_PIPE_AUTO && onepass_ok)) {
     if (!onepass_ok)
       return fail(FMCW_E_ARG, "single-pass schedule: needs nr 1024, pn == nd == 256, even nts <= nr, "
                               "complex64 in/out and no range cube");
@@ -594,9 +596,9 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const bool fusable = !d_cube && fmcw::fused_supported(NR, ND);
   if (c->pipe_mode == FMCW_PIPE_FUSED && !fusable)
     return fail(FMCW_E_ARG, "fused schedule: no fused kernel for this geometry, or a range cube was requested");
-  // AUTO = streams: with a 2 MiB fp32 range cube per frame two frames in
-  // flight do not fit one XCD's 4 MiB L2, so the fused schedule moves the same
-  // HBM bytes as the streams one and is slower (fused schedule)
+  // otherwise AUTO = streams: with a 2 MiB fp32 range cube per frame two frames
+  // in flight do not fit one XCD's 4 MiB L2, so the fused schedule moves the
+  // same HBM bytes as the streams one and is slower (fused schedule)
   if (fusable && c->pipe_mode == FMCW_PIPE_FUSED)
     return process_fused(c, p, d_iq, in_dtype, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd,
                          d_rd ? out_dtype : FMCW_C64, probe_column, d_probe, s);

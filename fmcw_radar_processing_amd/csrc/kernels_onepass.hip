@@ -242,7 +242,7 @@ __device__ __forceinline__ void dft32p(c2 (&v)[32]) {
 // LDS image of k_rd1p.
 struct Lds1p {
   c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the corner turn
-  f4v gh[128];             // {Gh, Hh} of bin t + 8 m at [m]
+  f4v gh0[64], gh1[64];    // {Gh, Hh} of lane l's bins r0(l), r1(l) (lane order: conflict-free reads)
   float red[2][NW][3][64]; // per-wave {sum.re, sum.im, max |X|^2} of each row over the wave's chirps
 };
 
@@ -266,7 +266,10 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   if (f >= a.F) return;                          // block-uniform
   const int S = FULL ? NR : a.S;
 
-  if (tid < 128) L.gh[tid] = reinterpret_cast<const f4v*>(a.gh)[t + 8 * tid];
+  if (tid < 128) {
+    const int m = bitrev6(lane) + (tid >> 6) * 64;
+    (tid < 64 ? L.gh0 : L.gh1)[lane] = reinterpret_cast<const f4v*>(a.gh)[t + 8 * m];
+  }
   // stage-A constants c_t[n] = w'[n] W1024^(t n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
   c2 cst[16];
 #pragma unroll
@@ -342,7 +345,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     // :204 the chirp mean, applied to the spectrum: X -= Gh + mean(x) Hh
     const c2 sx = s4.xy + s4.zw;
     const c2 nmx = c2{wave_sum(sx.x), wave_sum(sx.y)} * ninvS;
-    const f4v g0 = L.gh[m0], g1 = L.gh[m0 + 64];
+    const f4v g0 = L.gh0[lane], g1 = L.gh1[lane];
     const c2 ow = cmv(A1, w128);
     const c2 X0 = cmac_a(A0 + ow - g0.xy, nmx, g0.zw);   // bin r0 of chirp k
     const c2 X1 = cmac_a(A0 - ow - g1.xy, nmx, g1.zw);   // bin r1
@@ -470,9 +473,19 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       const int r = t + 8 * bitrev6(lb) + 512 * sl;
       // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element e = d2o + 32 d1s
       if (a.rd) {                                // RD written: k_detect_1p reads the target rows' peaks from it
-        c2* __restrict__ out = reinterpret_cast<c2*>(a.rd + (f * NR + r) * (int64_t)ND);
+        // 16-byte stores: lane pairs (d2o even / odd) swap one value per d1s pair,
+        // the even lane then writes elements (d2o, d2o + 1) of d1s = 2m, the odd
+        // lane those of d1s = 2m + 1: 512 contiguous bytes per row and instruction
+        f4v* __restrict__ out = reinterpret_cast<f4v*>(a.rd + (f * NR + r) * (int64_t)ND);
+        const bool odd = d2o & 1;
 #pragma unroll
-        for (int d1s = 0; d1s < NW; ++d1s) out[d2o + CPW * d1s] = v[(d1s + NW / 2) & (NW - 1)];
+        for (int m = 0; m < NW / 2; ++m) {
+          const c2 A = v[(2 * m + NW / 2) & (NW - 1)], B = v[(2 * m + 1 + NW / 2) & (NW - 1)];
+          const c2 snd = odd ? A : B;
+          const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
+          const int e = (d2o & ~1) + CPW * (2 * m + (odd ? 1 : 0));
+          out[e >> 1] = odd ? f4v{rcv.x, rcv.y, B.x, B.y} : f4v{A.x, A.y, rcv.x, rcv.y};
+        }
         continue;
       }
       // :233 [val, di] = max(abs(.)): exact max of |D|^2 over the row, then its first index

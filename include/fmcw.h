@@ -215,10 +215,12 @@ int fmcw_timing_reset(fmcw_ctx* ctx);
  * 0 restores the default. */
 int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
 
-/* Schedule of fmcw_process_device / fmcw_process (results are identical):
- *  FMCW_PIPE_AUTO    currently the streams schedule (default; see DESIGN.md:
- *                    at 2 MiB of fp32 range cube per frame the fused schedule
- *                    cannot keep its slots in L2 and is slower);
+/* Schedule of fmcw_process_device / fmcw_process (streams and fused give
+ * identical bits; the single pass agrees with them to fp32 rounding):
+ *  FMCW_PIPE_AUTO    the single pass where it applies (geometry below, no
+ *                    range cube requested), else the streams schedule (at
+ *                    2 MiB of fp32 range cube per frame the fused schedule
+ *                    cannot keep its slots in L2 and is slower; DESIGN.md);
  *  FMCW_PIPE_STREAMS K1 | K2 | K3 kernels as a 3-stream chunk pipeline, the
  *                    range cube of each chunk round-trips through HBM;
  *  FMCW_PIPE_FUSED   one persistent kernel per call: each XCD runs its frames'
