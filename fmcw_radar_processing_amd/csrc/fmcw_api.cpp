@@ -95,7 +95,7 @@ struct fmcw_ctx {
   int pipe_mode = FMCW_PIPE_AUTO, pipe_nslot = 2;
   DevBuf fused_ctrl, fused_slots, fused_rd_slots, fused_sticky;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
-  DevBuf op_gh;                                // single-pass: {Gh, Hh} per range bin
+  DevBuf op_gh, op_tab;                        // single-pass tables (fmcw::OP_TAB_*)
   float op_gh_scale = 0.f;                     // IF_scale op_gh was built for (0 = stale)
   bool fused_ran = false;
   int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
@@ -470,7 +470,7 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
     gr[i] = ((double)c->h_cal[2 * i] - mr) * wf[i];
     gi[i] = ((double)c->h_cal[2 * i + 1] - mi) * wf[i];
   }
-  std::vector<float> t(4 * (size_t)NR);
+  std::vector<float> t(4 * (size_t)NR), g(4 * (size_t)NR);
   for (int r = 0; r < NR; ++r) {
     double Gr = 0, Gi = 0, Hr = 0, Hi = 0;
     for (int i = 0, idx = 0; i < n; ++i, idx = (idx + r) & (NR - 1)) {
@@ -481,8 +481,43 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
     }
     t[4 * r] = (float)Gr; t[4 * r + 1] = (float)Gi; t[4 * r + 2] = (float)Hr; t[4 * r + 3] = (float)Hi;
   }
-  CHK(c->op_gh.ensure(t.size() * 4));
-  HIPCHK(hipMemcpyAsync(c->op_gh.p, t.data(), t.size() * 4, hipMemcpyHostToDevice, s));
+  // lane order of k_rd1p: [tile t][slot s][lane l] holds bin t + 8 (bitrev6(l) + 64 s)
+  auto bitrev6 = [](int l) { int r = 0; for (int i = 0; i < 6; ++i) r |= ((l >> i) & 1) << (5 - i); return r; };
+  for (int tt = 0; tt < fmcw::OP_TILES; ++tt)
+    for (int sl = 0; sl < 2; ++sl)
+      for (int l = 0; l < 64; ++l) {
+        const int r = tt + 8 * (bitrev6(l) + 64 * sl), o = ((tt * 2 + sl) * 64 + l) * 4;
+        for (int q = 0; q < 4; ++q) g[o + q] = t[4 * r + q];
+      }
+  std::vector<float> tab(2 * (size_t)fmcw::OP_TAB_SIZE);
+  auto put = [&](int idx, double re, double im) { tab[2 * idx] = (float)re; tab[2 * idx + 1] = (float)im; };
+  for (int l = 0; l < 64; ++l) {
+    for (int i = 0; i < 5; ++i) {            // span hh = 32 >> i: W_{2 hh}^(l mod hh) on set lanes
+      const int hh = 32 >> i;
+      const int e = (l & hh) ? ((l & (hh - 1)) * (512 / hh)) & (NR - 1) : 0;
+      put(fmcw::OP_TAB_LANE + i * 64 + l, cr[e], ci[e]);
+    }
+    const int e = 8 * bitrev6(l);
+    put(fmcw::OP_TAB_LANE + 5 * 64 + l, cr[e], ci[e]);
+  }
+  for (int i = 0; i < 8; ++i)
+    for (int d = 0; d < 32; ++d) {
+      const double a = -2.0 * M_PI * (double)((i * d) & 255) / 256.0;
+      put(fmcw::OP_TAB_TWR + i * 32 + d, std::cos(a), std::sin(a));
+    }
+  for (int tt = 0; tt < 8; ++tt)
+    for (int j = 0; j < 8; ++j)
+      for (int e = 0; e < 2; ++e)
+        for (int l = 0; l < 64; ++l) {
+          const int nn = 2 * l + e + 128 * j, idx = (tt * nn) & (NR - 1);
+          const double wv = nn < n ? wf[nn] : 0.0;
+          put(fmcw::OP_TAB_CST + ((tt * 8 + j) * 2 + e) * 64 + l, (double)(float)cr[idx] * wv,
+              (double)(float)ci[idx] * wv);
+        }
+  CHK(c->op_gh.ensure(g.size() * 4));
+  HIPCHK(hipMemcpyAsync(c->op_gh.p, g.data(), g.size() * 4, hipMemcpyHostToDevice, s));
+  CHK(c->op_tab.ensure(tab.size() * 4));
+  HIPCHK(hipMemcpyAsync(c->op_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
   c->op_gh_scale = if_scale;
   return FMCW_OK;
@@ -523,6 +558,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.F = nf; a.C = C; a.S = S;
     a.calw = c->calw.as<float4>();
     a.gh = c->op_gh.as<float4>();
+    a.tab = c->op_tab.as<float2>();
     a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
     a.rd = d_rd ? static_cast<float2*>(d_rd) + (size_t)f0 * NR * ND : nullptr;
     a.profile = d_prof + f0 * NR;

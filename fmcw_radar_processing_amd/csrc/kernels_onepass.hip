@@ -266,20 +266,18 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   if (f >= a.F) return;                          // block-uniform
   const int S = FULL ? NR : a.S;
 
-  if (tid < 128) {
-    const int m = bitrev6(lane) + (tid >> 6) * 64;
-    (tid < 64 ? L.gh0 : L.gh1)[lane] = reinterpret_cast<const f4v*>(a.gh)[t + 8 * m];
-  }
+  // Per-tile tables come from host-built arrays laid out in lane order
+  // (fmcw_api.cpp build_onepass_gh), so every table read is a coalesced
+  // 512-byte wave access: gathers here would cost the L2 as many requests as
+  // the frame itself.
+  const c2* __restrict__ tab = reinterpret_cast<const c2*>(a.tab);
+  if (tid < 128) (tid < 64 ? L.gh0 : L.gh1)[lane] = reinterpret_cast<const f4v*>(a.gh)[(2 * t + (tid >> 6)) * 64 + lane];
   // stage-A constants c_t[n] = w'[n] W1024^(t n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
   c2 cst[16];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int n = 2 * lane + e + 128 * j;
-      const float wv = n < S ? a.calw[n].z : 0.f;
-      cst[2 * j + e] = tov(a.tw_nr[(t * n) & (NR - 1)]) * wv;
-    }
+    for (int e = 0; e < 2; ++e) cst[2 * j + e] = tab[OP_TAB_CST + ((t * 8 + j) * 2 + e) * 64 + lane];
   c2 cs7[2];                                     // rotated copies for the last, compiler-visible MAC
   cs7[0] = c2{-cst[14].y, cst[14].x};
   cs7[1] = c2{-cst[15].y, cst[15].x};
@@ -289,10 +287,10 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   for (int i = 0; i < 6; ++i) {
     const int hh = 32 >> i;
     sg[i] = (lane & hh) ? -1.f : 1.f;
-    if (i < 5) twh[i] = (lane & hh) ? tov(a.tw_nr[((lane & (hh - 1)) * (512 / hh)) & (NR - 1)]) : c2{1.f, 0.f};
+    if (i < 5) twh[i] = tab[OP_TAB_LANE + i * 64 + lane];
   }
   const int m0 = bitrev6(lane);
-  const c2 w128 = tov(a.tw_nr[8 * m0]);
+  const c2 w128 = tab[OP_TAB_LANE + 5 * 64 + lane];
   const int r0 = t + 8 * m0, r1 = r0 + 512;      // this lane's two range bins
   __syncthreads();
 
@@ -437,7 +435,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   const int d2o = tid & 31;
   c2 twr[NW];                                    // W256^(i d2o): the inter-stage twiddle, applied by the reader
 #pragma unroll
-  for (int i = 1; i < NW; ++i) twr[i] = tov(a.tw_nd[(i * d2o) & (ND - 1)]);
+  for (int i = 1; i < NW; ++i) twr[i] = tab[OP_TAB_TWR + i * 32 + d2o];
   // max / min over the 32 lanes of a row (DPP: xor 1, xor 2, then mirrors on
   // group-uniform values, then the 16-lane row swap)
   auto row_max = [&](int v) {

@@ -4,18 +4,18 @@
 // Each workgroup = one tile of one frame (blocks 64j + 8t + x: the 8 tiles of
 // frame 8j + x on XCD x), NW waves, each wave streams chirps w + NW k2 of the
 // frame (8 x 16-byte loads per lane per chirp), DEPTH chirps in flight, and
-// only sums what it loads.  Optional stagger: tile t starts STAG*t chirps
-// later (mod C).  Prints the L2->CU read rate (8 reads per frame) and the
-// frame rate.
+// sums what it loads; WORK extra packed FMAs per chirp stand in for the
+// range-FFT arithmetic.  Optional stagger: tile t starts STAG*t chirps later
+// (mod C).  Prints the L2->CU read rate (8 reads per frame) and the frame rate.
 //
-//   hipcc --offload-arch=gfx950 -O3 tools/l2_probe.hip -o /tmp/l2_probe && /tmp/l2_probe
+//   hipcc --offload-arch=gfx950 -O3 tools/l2_probe.hip -o tools/l2_probe.bin && tools/l2_probe.bin
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-template <int NW, int DEPTH, int LDSKB>
+template <int NW, int DEPTH, int LDSKB, int WORK>
 __global__ __launch_bounds__(64 * NW, 1) void k_read(const f4v* __restrict__ iq, int F, int C, int stag, float* out) {
   __shared__ float pad[LDSKB * 256];             // occupancy as the real kernel (1 workgroup per CU)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, b = blockIdx.x;
@@ -37,46 +37,60 @@ __global__ __launch_bounds__(64 * NW, 1) void k_read(const f4v* __restrict__ iq,
 #pragma unroll
   for (int i = 0; i < cpw; ++i) {
     if (i + DEPTH - 1 < cpw) ld(i + DEPTH - 1, buf[(i + DEPTH - 1) % DEPTH]);
+    f4v s = buf[i % DEPTH][0];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc += buf[i % DEPTH][j];
+    for (int j = 1; j < 8; ++j) s += buf[i % DEPTH][j];
+    // WORK packed FMAs per chirp in 4 independent chains (2 per f4v op)
+    f4v u0 = s, u1 = s * 1.5f;
+#pragma unroll
+    for (int q = 0; q < WORK / 4; ++q) {
+      u0 = u0 * 0.999f + 0.5f;
+      u1 = u1 * 0.998f + 0.25f;
+    }
+    acc += u0 + u1;
   }
   if (acc.x == 1234.5f) { pad[threadIdx.x] = acc.y; out[b] = pad[(threadIdx.x + 1) % 64]; }
 }
 
-template <int NW, int DEPTH, int LDSKB>
+template <int NW, int DEPTH, int LDSKB, int WORK>
 void run(const char* name, const f4v* d, int F, int C, int stag, float* o) {
   const int blocks = ((F + 7) / 8) * 64;
   hipEvent_t a, e;
-  hipEventCreate(&a);
-  hipEventCreate(&e);
-  k_read<NW, DEPTH, LDSKB><<<blocks, 64 * NW>>>(d, F, C, stag, o);
-  hipEventRecord(a);
+  (void)hipEventCreate(&a);
+  (void)hipEventCreate(&e);
+  k_read<NW, DEPTH, LDSKB, WORK><<<blocks, 64 * NW>>>(d, F, C, stag, o);
+  (void)hipEventRecord(a);
   const int reps = 5;
-  for (int r = 0; r < reps; ++r) k_read<NW, DEPTH, LDSKB><<<blocks, 64 * NW>>>(d, F, C, stag, o);
-  hipEventRecord(e);
-  hipEventSynchronize(e);
+  for (int r = 0; r < reps; ++r) k_read<NW, DEPTH, LDSKB, WORK><<<blocks, 64 * NW>>>(d, F, C, stag, o);
+  (void)hipEventRecord(e);
+  (void)hipEventSynchronize(e);
   float ms = 0;
-  hipEventElapsedTime(&ms, a, e);
+  (void)hipEventElapsedTime(&ms, a, e);
   ms /= reps;
   const double bytes = (double)F * C * 8192.0;
   printf("%-28s stag %d: %.3f ms  L2->CU %.1f TB/s  frames %.3f M/s (HBM-once %.2f TB/s)\n", name, stag, ms,
          8 * bytes / ms / 1e9, F / ms / 1e3, bytes / ms / 1e9);
 }
 
+__global__ void k_fill(f4v* d, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    d[i] = f4v{(float)(i & 1023), 1.f, -0.5f, (float)(i >> 20)};
+}
+
 int main() {
   const int F = 4096, C = 256;
   f4v* d;
   float* o;
-  hipMalloc(&d, (size_t)F * C * 8192);
-  hipMalloc(&o, 1 << 20);
-  hipMemset(d, 0, (size_t)F * C * 8192);
-  run<8, 3, 128>("nw8 depth3 (kernel)", d, F, C, 0, o);
-  run<8, 3, 128>("nw8 depth3 (kernel)", d, F, C, 1, o);
-  for (int ff : {256, 64, 32, 16, 8}) {
-    char nm[64];
-    snprintf(nm, sizeof nm, "nw8 depth3 F=%d", ff);
-    run<8, 3, 128>(nm, d, ff, C, 1, o);
-  }
-  run<8, 3, 60>("nw8 depth3 2 WG/CU", d, F, C, 1, o);
+  (void)hipMalloc(&d, (size_t)F * C * 8192);
+  (void)hipMalloc(&o, 1 << 20);
+  k_fill<<<4096, 256>>>(d, (size_t)F * C * 512);
+  run<8, 3, 128, 0>("nw8 depth3", d, F, C, 0, o);
+  run<8, 3, 128, 64>("nw8 depth3 work64", d, F, C, 0, o);
+  run<8, 3, 128, 160>("nw8 depth3 work160", d, F, C, 0, o);
+  run<8, 3, 128, 320>("nw8 depth3 work320", d, F, C, 0, o);
+  run<8, 3, 128, 0>("nw8 depth3 F=32", d, 32, C, 0, o);
+  run<8, 3, 128, 160>("nw8 depth3 work160 F=32", d, 32, C, 0, o);
+  run<8, 3, 128, 0>("nw8 depth3 stag1", d, F, C, 1, o);
+  run<8, 3, 60, 0>("nw8 depth3 2 WG/CU", d, F, C, 0, o);
   return 0;
 }
