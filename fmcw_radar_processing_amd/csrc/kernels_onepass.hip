@@ -244,6 +244,7 @@ struct Lds1p {
   c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the corner turn
   f4v gh0[64], gh1[64];    // {Gh, Hh} of lane l's bins r0(l), r1(l) (lane order: conflict-free reads)
   float red[2][NW][3][64]; // per-wave {sum.re, sum.im, max |X|^2} of each row over the wave's chirps
+  float cand[OP_CAND][256];// candidate rows |X|^2 as [wave][k2] (chirp w + 8 k2), written out coalesced
 };
 
 }  // namespace op
@@ -390,6 +391,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   }
 
   // ---------------- slow-time candidates (:257-259) -------------------------
+  int csel[OP_CAND];
   {
     const double dpb = a.dist_per_bin, lo = a.min_d, hi = a.max_d;
     auto key = [&](int r, float p) {
@@ -407,15 +409,19 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       if (w == 0 && lane == 0) a.cand_idx[(f * OP_TILES + t) * OP_CAND + c] = sel;
       // |X[sel, k]|^2 of the candidate row (k_detect_1p takes the square root of
       // the one row it keeps); the slot is wave-uniform (r1 = r0 + 512)
-      float* row = a.cand_rows + ((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C;
+      // (staged in LDS by the owning lane, stored coalesced after the next barrier)
+      csel[c] = sel;
+      f4v* crow = reinterpret_cast<f4v*>(&L.cand[c][w * CPW]);
       if (sel >= 512) {
         if (r1 == sel)
 #pragma unroll
-          for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = abs2v(tile1[k2]);
+          for (int q = 0; q < CPW / 4; ++q)
+            crow[q] = f4v{abs2v(tile1[4 * q]), abs2v(tile1[4 * q + 1]), abs2v(tile1[4 * q + 2]), abs2v(tile1[4 * q + 3])};
       } else if (sel >= 0) {
         if (r0 == sel)
 #pragma unroll
-          for (int k2 = 0; k2 < CPW; ++k2) row[w + NW * k2] = abs2v(tile0[k2]);
+          for (int q = 0; q < CPW / 4; ++q)
+            crow[q] = f4v{abs2v(tile0[4 * q]), abs2v(tile0[4 * q + 1]), abs2v(tile0[4 * q + 2]), abs2v(tile0[4 * q + 3])};
       }
       if (r0 == sel) v0 = -1.f;
       if (r1 == sel) v1 = -1.f;
@@ -505,7 +511,11 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   pre(tile0, mu0);
   pre(tile1, mu1);
   stage(tile0);
-  __syncthreads();                               // B3: slot-0 corner turn written
+  __syncthreads();                               // B3: slot-0 corner turn written (and the candidate rows)
+#pragma unroll
+  for (int c = 0; c < OP_CAND; ++c)
+    if (csel[c] >= 0 && tid < C)
+      a.cand_rows[((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C + tid] = L.cand[c][(tid % NW) * CPW + tid / NW];
   post(0);
   __syncthreads();                               // B4: slot-0 corner turn read out
   stage(tile1);
