@@ -309,17 +309,18 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     }
   };
   c2 tile0[CPW];                                 // slot 1 goes to LDS (L.t1)
-  f4v buf[3][8];                                 // chirp ring: 2 chirps in flight while one is consumed
+  // chirp ring: the next chirp is in flight while one is consumed (a deeper
+  // ring measured no faster: the VGPRs are worth more than the prefetch depth)
+  f4v buf[2][8];
   ld_chirp(w, buf[0]);
-  ld_chirp(w + NW, buf[1]);
 #pragma unroll
   for (int k2 = 0; k2 < CPW; ++k2) {
     const int k = w + NW * k2;
-    if (k2 + 2 < CPW) ld_chirp(k + 2 * NW, buf[(k2 + 2) % 3]);
+    if (k2 + 1 < CPW) ld_chirp(k + NW, buf[(k2 + 1) % 2]);
     f4v x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      x[j] = buf[k2 % 3][j];
+      x[j] = buf[k2 % 2][j];
       if constexpr (!FULL)
         if (!(lane + 64 * j < S2)) x[j] = f4v{0.f, 0.f, 0.f, 0.f};
     }
@@ -509,8 +510,8 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     }
   };
   pre(tile0, mu0);
+  stage(tile0);                                  // L.t1 was read out before B2; tile0 dies here
   pre(tile1, mu1);
-  stage(tile0);
   __syncthreads();                               // B3: slot-0 corner turn written (and the candidate rows)
 #pragma unroll
   for (int c = 0; c < OP_CAND; ++c)
