@@ -135,6 +135,29 @@ __device__ __forceinline__ float wave_sum(float v) {
   return lo + hi;
 }
 
+// Wave-wide max / min of an int by DPP and the two half swaps (no LDS
+// round trips): xor 1, xor 2, then the mirrors on group-uniform values, then
+// the 16- and 32-lane swaps.  Every lane ends with the result.
+template <bool MAX> __device__ __forceinline__ int wave_red_i(int v) {
+  auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+  v = op(v, dppi<0xB1>(v));
+  v = op(v, dppi<0x4E>(v));
+  v = op(v, dppi<0x141>(v));
+  v = op(v, dppi<0x140>(v));
+  auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+  v = op((int)r[0], (int)r[1]);
+  r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+  return op((int)r[0], (int)r[1]);
+}
+// wave_argmax for keys that are either > 0 or -1 (frame_ops.h rule: largest
+// value, ties -> lowest index): positive floats order as their int bits.
+__device__ __forceinline__ void wave_argmax_dpp(float& v, int& i) {
+  const int key = v < 0.f ? -1 : __float_as_int(v);
+  const int m = wave_red_i<true>(key);
+  i = wave_red_i<false>(key == m ? i : INT_MAX);
+  v = m < 0 ? -1.f : __int_as_float(m);
+}
+
 // One radix-2 DIF stage of span H across lanes: bit-H-clear lane -> a + b,
 // bit-H-set lane -> (a - b) * tw.  sg = -1 on set lanes, +1 on clear lanes.
 template <int H>
@@ -405,7 +428,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       float bv = v0;
       int bi = r0;
       if (v1 > bv) { bv = v1; bi = r1; }                           // r0 < r1: ties keep r0
-      wave_argmax(bv, bi);                                          // same result in every wave
+      wave_argmax_dpp(bv, bi);                                      // same result in every wave
       const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
       if (w == 0 && lane == 0) a.cand_idx[(f * OP_TILES + t) * OP_CAND + c] = sel;
       // |X[sel, k]|^2 of the candidate row (k_detect_1p takes the square root of
