@@ -534,13 +534,13 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   };
   pre(tile0, mu0);
   stage(tile0);                                  // L.t1 was read out before B2; tile0 dies here
-  pre(tile1, mu1);
   __syncthreads();                               // B3: slot-0 corner turn written (and the candidate rows)
 #pragma unroll
   for (int c = 0; c < OP_CAND; ++c)
     if (csel[c] >= 0 && tid < C)
       a.cand_rows[((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C + tid] = L.cand[c][(tid % NW) * CPW + tid / NW];
-  post(0);
+  post(0);                                       // its LDS reads and stores overlap slot 1's DFT arithmetic
+  pre(tile1, mu1);
   __syncthreads();                               // B4: slot-0 corner turn read out
   stage(tile1);
   __syncthreads();                               // B5
