@@ -481,23 +481,24 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
     }
     t[4 * r] = (float)Gr; t[4 * r + 1] = (float)Gi; t[4 * r + 2] = (float)Hr; t[4 * r + 3] = (float)Hi;
   }
-  // lane order of k_rd1p: [tile t][slot s][lane l] holds bin t + 8 (bitrev6(l) + 64 s)
-  auto bitrev6 = [](int l) { int r = 0; for (int i = 0; i < 6; ++i) r |= ((l >> i) & 1) << (5 - i); return r; };
+  // lane order of k_rd1p: [tile t][slot s][lane l] holds bin t + 8 (lane_bin(l) + 64 s),
+  // lane_bin(l) = 4 bitrev4(l mod 16) + l / 16 (kernels_onepass.hip)
+  auto lane_bin = [](int l) { int r = 0; for (int i = 0; i < 4; ++i) r |= ((l >> i) & 1) << (5 - i); return r + (l >> 4); };
   for (int tt = 0; tt < fmcw::OP_TILES; ++tt)
     for (int sl = 0; sl < 2; ++sl)
       for (int l = 0; l < 64; ++l) {
-        const int r = tt + 8 * (bitrev6(l) + 64 * sl), o = ((tt * 2 + sl) * 64 + l) * 4;
+        const int r = tt + 8 * (lane_bin(l) + 64 * sl), o = ((tt * 2 + sl) * 64 + l) * 4;
         for (int q = 0; q < 4; ++q) g[o + q] = t[4 * r + q];
       }
   std::vector<float> tab(2 * (size_t)fmcw::OP_TAB_SIZE);
   auto put = [&](int idx, double re, double im) { tab[2 * idx] = (float)re; tab[2 * idx + 1] = (float)im; };
   for (int l = 0; l < 64; ++l) {
-    for (int i = 0; i < 5; ++i) {            // span hh = 32 >> i: W_{2 hh}^(l mod hh) on set lanes
-      const int hh = 32 >> i;
-      const int e = (l & hh) ? ((l & (hh - 1)) * (512 / hh)) & (NR - 1) : 0;
+    for (int i = 0; i < 5; ++i) {            // span hh = 32 >> i: W_{2 hh}^(l mod hh), on every lane for the
+      const int hh = 32 >> i;                // pair butterflies (spans 32, 16), on set lanes for spans 8, 4, 2
+      const int e = (hh >= 16 || (l & hh)) ? ((l & (hh - 1)) * (512 / hh)) & (NR - 1) : 0;
       put(fmcw::OP_TAB_LANE + i * 64 + l, cr[e], ci[e]);
     }
-    const int e = 8 * bitrev6(l);
+    const int e = 8 * lane_bin(l);
     put(fmcw::OP_TAB_LANE + 5 * 64 + l, cr[e], ci[e]);
   }
   for (int i = 0; i < 8; ++i)

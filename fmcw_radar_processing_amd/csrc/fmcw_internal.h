@@ -104,7 +104,7 @@ inline int64_t fused_ctrl_words(int64_t F) { return 256 + 3 * F + 1; }
 constexpr int OP_TILES = 8;
 constexpr int OP_CAND = 2;           // slow-time candidate rows kept per tile
 // Single-pass table (float2), lane-ordered sections:
-constexpr int OP_TAB_LANE = 0;       // [6][64]: DIF twiddles of spans 32..2 (1 on clear lanes), W128^bitrev6(l)
+constexpr int OP_TAB_LANE = 0;       // [6][64]: DIF twiddles of spans 32..2 (1 on clear lanes of spans 8..2), W128^lane_bin(l)
 constexpr int OP_TAB_TWR = 384;      // [8][32]: W256^(i d2)
 constexpr int OP_TAB_CST = 640;      // [8 t][8 j][2 e][64 l]: w'[n] W1024^(t n), n = 2l + e + 128j
 constexpr int OP_TAB_SIZE = 640 + 8 * 1024;
@@ -114,7 +114,7 @@ struct OnePassArgs {
   int64_t F;
   int C, S;                // NR = 1024, ND = C (kernel template)
   const float4* calw;      // [S] {cal.re, cal.im, IF_scale*w, w}
-  const float4* gh;        // [8 t][2 s][64 l] {Gh, Hh} of bin t + 8 (bitrev6(l) + 64 s):
+  const float4* gh;        // [8 t][2 s][64 l] {Gh, Hh} of bin t + 8 (lane_bin(l) + 64 s):
                            // DFT((cal - mean(cal)) w') and DFT(w') (host, float64)
   const float2* tab;       // OP_TAB_* sections (host, float64, lane order)
   const float2* tw_nr;     // [NR]

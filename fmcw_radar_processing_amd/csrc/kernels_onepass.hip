@@ -34,8 +34,9 @@
 //
 // Per chirp (one wave, 16 samples per lane as 8 float4 loads, lane l holds
 // a = 2l and 2l+1): stage A, a 64-point cross-lane DIF FFT on each of the two
-// sub-sequences (DPP and v_permlane16/32_swap exchanges, no LDS), one in-lane
-// radix-2 -> bins r(l, s) = t + 8 (bitrev6(l) + 64 s), s = 0, 1, then the
+// sub-sequences (spans 32 and 16 as pair butterflies over v_permlane32/16_swap
+// of the two registers, spans 8..1 by DPP, no LDS), one in-lane radix-2 ->
+// bins r(l, s) = t + 8 (lane_bin(l) + 64 s), s = 0, 1, then the
 // Gh/Hh correction.  Loads run two chirps ahead (a 3-deep register ring).
 // Wave w handles chirps k = w + 8 k2 (k2 < 32): slot 0 in VGPRs, slot 1 in LDS.
 //
@@ -185,7 +186,51 @@ __device__ __forceinline__ float2 sload(const float2* p, int i) {
   return make_float2(v.x, v.y);
 }
 
-__device__ __forceinline__ int bitrev6(int l) { return (int)(__brev((unsigned)l) >> 26); }
+// Sub-bin m (r = t + 8 m) of lane l's slot-0 value after the range FFT below:
+// 4 bitrev4(l mod 16) + l / 16 (the two pair stages leave the four 16-point
+// sub-FFTs of each half-sequence in the four 16-lane rows).
+__device__ __forceinline__ int lane_bin(int l) { return (int)(__brev((unsigned)(l & 15)) >> 26) + (l >> 4); }
+
+// Pair butterfly of span H (32 or 16) on two registers: one half swap per
+// component gives every lane both operands of one butterfly (no copies), and it
+// keeps both outputs: R0 <- lo + hi, R1 <- (lo - hi) * tw.  Lane l < H-block
+// handles R0's pair, the other block R1's pair (see lane_bin).
+template <int H> __device__ __forceinline__ void pair_bfly(c2& R0, c2& R1, c2 tw) {
+  const auto rx = H == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.x), __float_as_uint(R1.x), false, false)
+                          : __builtin_amdgcn_permlane16_swap(__float_as_uint(R0.x), __float_as_uint(R1.x), false, false);
+  const auto ry = H == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.y), __float_as_uint(R1.y), false, false)
+                          : __builtin_amdgcn_permlane16_swap(__float_as_uint(R0.y), __float_as_uint(R1.y), false, false);
+  const c2 lo = c2{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+  const c2 hi = c2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+  R0 = lo + hi;
+  R1 = cmv(lo - hi, tw);
+}
+// The final half swap without arithmetic: lane l then holds (E[m], O[m]) of
+// one sub-bin m = lane_bin(l).
+__device__ __forceinline__ void pair_swap32(c2& R0, c2& R1) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.x), __float_as_uint(R1.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.y), __float_as_uint(R1.y), false, false);
+  R0 = c2{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
+  R1 = c2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
+}
+
+// Wave-wide complex sum, every lane gets it.  The 16-lane swap of re against im
+// first puts re partials in rows 0, 2 and im partials in rows 1, 3 of ONE
+// register, so the four DPP levels run once (symmetric pairings: identical bits
+// in every lane of a row), then the 32-lane swap adds the row pairs and a last
+// 16-lane swap spreads re and im to every lane.
+__device__ __forceinline__ c2 wave_sum_c(c2 s) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s.x), __float_as_uint(s.y), false, false);
+  float v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  const auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  const float u = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+  const auto z = __builtin_amdgcn_permlane16_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+  return c2{__uint_as_float(z[0]), __uint_as_float(z[1])};
+}
 
 // ---- packed small DFTs (natural order in and out) ------------------------
 __device__ __forceinline__ void dft4p(c2& a0, c2& a1, c2& a2, c2& a3) {
@@ -305,7 +350,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   c2 cs7[2];                                     // rotated copies for the last, compiler-visible MAC
   cs7[0] = c2{-cst[14].y, cst[14].x};
   cs7[1] = c2{-cst[15].y, cst[15].x};
-  c2 twh[5];                                     // spans 32, 16, 8, 4, 2 (1 on clear lanes)
+  c2 twh[5];                                     // spans 32, 16 (every lane), 8, 4, 2 (1 on clear lanes)
   float sg[6];                                   // spans 32 .. 1
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
@@ -313,7 +358,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     sg[i] = (lane & hh) ? -1.f : 1.f;
     if (i < 5) twh[i] = tab[OP_TAB_LANE + i * 64 + lane];
   }
-  const int m0 = bitrev6(lane);
+  const int m0 = lane_bin(lane);
   const c2 w128 = tab[OP_TAB_LANE + 5 * 64 + lane];
   const int r0 = t + 8 * m0, r1 = r0 + 512;      // this lane's two range bins
   __syncthreads();
@@ -359,15 +404,15 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     A0 = cmacv(A0, x[7].xy, cst[14], cs7[0]);   // compiler-visible producer for the DPP stages
     A1 = cmacv(A1, x[7].zw, cst[15], cs7[1]);
     s4 += x[7];
-    A0 = dif_stage<32>(A0, twh[0], sg[0]); A1 = dif_stage<32>(A1, twh[0], sg[0]);
-    A0 = dif_stage<16>(A0, twh[1], sg[1]); A1 = dif_stage<16>(A1, twh[1], sg[1]);
+    pair_bfly<32>(A0, A1, twh[0]);                // E = DFT64(A0), O = DFT64(A1): spans 32, 16 as pair
+    pair_bfly<16>(A0, A1, twh[1]);                // butterflies, then four 16-point DIFs per register
     A0 = dif_stage<8>(A0, twh[2], sg[2]);  A1 = dif_stage<8>(A1, twh[2], sg[2]);
     A0 = dif_stage<4>(A0, twh[3], sg[3]);  A1 = dif_stage<4>(A1, twh[3], sg[3]);
     A0 = dif_stage<2>(A0, twh[4], sg[4]);  A1 = dif_stage<2>(A1, twh[4], sg[4]);
     A0 = dif_stage<1>(A0, twh[4], sg[5]);  A1 = dif_stage<1>(A1, twh[4], sg[5]);
+    pair_swap32(A0, A1);                          // lane l: E[m], O[m], m = lane_bin(l)
     // :204 the chirp mean, applied to the spectrum: X -= Gh + mean(x) Hh
-    const c2 sx = s4.xy + s4.zw;
-    const c2 nmx = c2{wave_sum(sx.x), wave_sum(sx.y)} * ninvS;
+    const c2 nmx = wave_sum_c(s4.xy + s4.zw) * ninvS;
     const f4v g0 = L.gh0[lane], g1 = L.gh1[lane];
     const c2 ow = cmv(A1, w128);
     const c2 X0 = cmac_a(A0 + ow - g0.xy, nmx, g0.zw);   // bin r0 of chirp k
@@ -498,7 +543,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
 #pragma unroll
       for (int i = 1; i < NW; ++i) v[i] = cmul_a(v[i], twr[i]);
       dft8p(v);
-      const int r = t + 8 * bitrev6(lb) + 512 * sl;
+      const int r = t + 8 * lane_bin(lb) + 512 * sl;
       // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element e = d2o + 32 d1s
       if (a.rd) {                                // RD written: k_detect_1p reads the target rows' peaks from it
         // 16-byte stores: lane pairs (d2o even / odd) swap one value per d1s pair,
