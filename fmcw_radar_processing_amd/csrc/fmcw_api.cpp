@@ -529,7 +529,7 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
 // range cube; k_detect_1p runs the detection; k_slow_fix recomputes the rare
 // slow-time row that was not among a tile's candidates.  Chunks bound the
 // candidate scratch (OP_TILES*OP_CAND rows of PN floats per frame).
-static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int64_t F, float* d_prof,
+static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int h, int64_t F, float* d_prof,
                            int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
                            void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
   const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
@@ -546,7 +546,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   if (c->op_gh_scale != p->if_scale || !c->op_gh.p) CHK(build_onepass_gh(c, p->if_scale, s));
   if (pframe >= 0 && d_probe) {                // :410-411 fft_data column: one chirp by a direct DFT
     fmcw::ProbeArgs pa{};
-    pa.iq = static_cast<const float2*>(d_iq);
+    pa.iq = d_iq; pa.h = h;
     pa.frame = pframe; pa.chirp = pchirp; pa.C = C; pa.S = S; pa.NR = NR;
     pa.calw = c->calw.as<float4>(); pa.tw_nr = c->tw_nr.as<float2>(); pa.probe_mag = d_probe;
     HIPCHK(fmcw::launch_probe(pa, s));
@@ -555,13 +555,15 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   for (int64_t f0 = 0; f0 < F; f0 += chunk) {
     const int64_t nf = std::min(chunk, F - f0);
     fmcw::OnePassArgs a{};
-    a.iq = static_cast<const float2*>(d_iq) + (size_t)f0 * C * S;
+    a.iq = static_cast<const char*>(d_iq) + (size_t)f0 * C * S * (h ? 4 : 8);
+    a.h = h;
+    a.rd_scale = h ? 1.0f / ((float)NR * ND) : 1.0f;
     a.F = nf; a.C = C; a.S = S;
     a.calw = c->calw.as<float4>();
     a.gh = c->op_gh.as<float4>();
     a.tab = c->op_tab.as<float2>();
     a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
-    a.rd = d_rd ? static_cast<float2*>(d_rd) + (size_t)f0 * NR * ND : nullptr;
+    a.rd = d_rd ? static_cast<char*>(d_rd) + (size_t)f0 * NR * ND * (h ? 4 : 8) : nullptr;
     a.profile = d_prof + f0 * NR;
     a.rowpk = c->op_rowpk.as<int2>();
     a.cand_idx = c->op_cidx.as<int32_t>();
@@ -578,13 +580,13 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     }
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
     fmcw::Detect1pArgs k{};
-    k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
+    k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.rd_h = h; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
     k.nframes = (int)nf; k.NR = NR; k.C = C; k.M = M;
     k.det.ND = ND; k.det.C = C; k.det.M = M;
     k.det.range_thr = p->range_thr; k.det.doppler_thr = p->doppler_thr;
     k.det.min_d = p->min_d; k.det.max_d = p->max_d; k.det.dist_per_bin = p->dist_per_bin;
     k.det.fallback = p->doppler_fallback_idx;
-    k.det.cube_unscale = 1.0f; k.det.rd_unscale = 1.0f;
+    k.det.cube_unscale = 1.0f; k.det.rd_unscale = 1.0f / a.rd_scale;
     k.count = d_count + f0; k.ridx = d_ridx + f0 * M; k.rmag = d_rmag + f0 * M; k.didx = d_didx + f0 * M;
     k.slow_mag = d_slow + f0 * C;
     k.fix_list = fix_list; k.fix_count = fix_count;
@@ -594,7 +596,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       tm.done();
     }
     fmcw::SlowFixArgs x{};
-    x.iq = a.iq; x.C = C; x.S = S; x.NR = NR;
+    x.iq = a.iq; x.h = h; x.C = C; x.S = S; x.NR = NR;
     x.calw = a.calw; x.tw_nr = a.tw_nr;
     x.ridx = k.ridx; x.M = M;
     x.fix_list = fix_list; x.fix_count = fix_count;
@@ -619,15 +621,16 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
   if (probe_column < 0 || probe_column > F * (int64_t)C) return fail(FMCW_E_ARG, "probe_column out of range");
   hipStream_t s = pick(c, stream);
-  const bool onepass_ok = !d_cube && in_dtype == FMCW_C64 && (!d_rd || out_dtype == FMCW_C64) &&
-                          fmcw::onepass_supported(S, C, NR, ND);
+  // the single pass keeps one storage type end to end: c64 in / c64 RD, or
+  // fp16 storage (c32h in / c32h RD); the RD dtype is free when RD is not asked for
+  const bool onepass_ok = !d_cube && (!d_rd || out_dtype == in_dtype) && fmcw::onepass_supported(S, C, NR, ND);
   // AUTO = single pass wherever it applies: half the HBM bytes of the streams
   // schedule (no range cube) and faster on MI355X
   if (c->pipe_mode == FMCW_PIPE_ONEPASS || (c->pipe_mode == FMCW_PIPE_AUTO && onepass_ok)) {
     if (!onepass_ok)
       return fail(FMCW_E_ARG, "single-pass schedule: needs nr 1024, pn == nd == 256, even nts <= nr, "
-                              "complex64 in/out and no range cube");
-    return process_onepass(c, p, d_iq, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd, probe_column,
+                              "the RD map in the IQ dtype and no range cube");
+    return process_onepass(c, p, d_iq, in_dtype == FMCW_C32H ? 1 : 0, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd, probe_column,
                            d_probe, s);
   }
   const bool fusable = !d_cube && fmcw::fused_supported(NR, ND);

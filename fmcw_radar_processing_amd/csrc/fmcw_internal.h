@@ -110,7 +110,9 @@ constexpr int OP_TAB_CST = 640;      // [8 t][8 j][2 e][64 l]: w'[n] W1024^(t n)
 constexpr int OP_TAB_SIZE = 640 + 8 * 1024;
 
 struct OnePassArgs {
-  const float2* iq;        // [F][C][S] c64
+  const void* iq;          // [F][C][S] c64, or c32h when h
+  int h;                   // fp16 storage (FMCW_C32H): c32h IQ in, c32h RD out holding D / (NR ND)
+  float rd_scale;          // 1 / (NR ND) when h, else 1
   int64_t F;
   int C, S;                // NR = 1024, ND = C (kernel template)
   const float4* calw;      // [S] {cal.re, cal.im, IF_scale*w, w}
@@ -120,7 +122,7 @@ struct OnePassArgs {
   const float2* tw_nr;     // [NR]
   const float2* tw_nd;     // [ND]
   const float* wd;         // [C]
-  float2* rd;              // [F][NR][ND] or nullptr (then only the row peaks are kept)
+  void* rd;                // [F][NR][ND] c64 (c32h when h), or nullptr (then only the row peaks are kept)
   float* profile;          // [F][NR]
   int2* rowpk;             // [F][NR] {float bits of max_d |D[r,d]|, first argmax d (fftshift-ed, 0-based)}; only when rd is nullptr
   int32_t* cand_idx;       // [F][OP_TILES][OP_CAND] 0-based bin or -1
@@ -133,8 +135,8 @@ struct OnePassArgs {
 struct Detect1pArgs {
   const float* profile;    // [F][NR]
   const int2* rowpk;       // [F][NR] (used when rd is nullptr)
-  const float2* rd;        // [F][NR][ND] or nullptr
-  int ND;
+  const void* rd;          // [F][NR][ND] c64 (c32h when rd_h, holding D * det.rd_unscale^-1) or nullptr
+  int ND, rd_h;
   const int32_t* cand_idx; // [F][OP_TILES][OP_CAND]
   const float* cand_rows;  // [F][OP_TILES][OP_CAND][C] |X|^2
   int nframes, NR, C, M;
@@ -149,7 +151,8 @@ struct Detect1pArgs {
 };
 
 struct SlowFixArgs {
-  const float2* iq;        // [F][C][S]
+  const void* iq;          // [F][C][S] c64, or c32h when h
+  int h;
   int C, S, NR;
   const float4* calw;
   const float2* tw_nr;
@@ -165,7 +168,8 @@ hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s);
 hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s);
 
 struct ProbeArgs {          // fft_data column (:410-411) for the single-pass schedule
-  const float2* iq;        // [F][C][S] of the launch
+  const void* iq;          // [F][C][S] of the launch, c64 or c32h (h)
+  int h;
   int64_t frame;
   int chirp, C, S, NR;
   const float4* calw;

@@ -64,6 +64,13 @@ constexpr int NW = 8;                  // waves per workgroup (2 per SIMD: 256 V
 static_assert(NR / OP_TILES == 128, "the lane layout assumes a 128-point sub-FFT");
 
 using c2 = f2v;                        // complex (re, im) in a packed-fp32 register pair
+typedef _Float16 h4v __attribute__((ext_vector_type(4)));   // two fp16-storage samples (FMCW_C32H)
+
+// Sample i of an IQ buffer holding c64 (h = 0) or c32h (h = 1) values.
+__device__ __forceinline__ float2 ld_iq(const void* p, int64_t i, int h) {
+  if (h) return __half22float2(static_cast<const __half2*>(p)[i]);
+  return static_cast<const float2*>(p)[i];
+}
 
 // a * b in two packed ops: a.re * (b.re, b.im) + a.im * (-b.im, b.re)
 __device__ __forceinline__ c2 cmv(c2 a, c2 b) { return __builtin_elementwise_fma(a.yy, c2{-b.y, b.x}, a.xx * b); }
@@ -321,7 +328,7 @@ struct Lds1p {
 // k_rd1p: one workgroup (8 waves, 2 per SIMD, 256 VGPRs per lane) = one range
 // tile of one frame.  FULL: S == NR (no zero padding, no masking).
 // ---------------------------------------------------------------------------
-template <bool FULL>
+template <bool FULL, bool H>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
 __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   using namespace op;
   constexpr int CPW = 32, C = NW * CPW, ND = C;  // wave w owns chirps w + 8 k2, k2 < 32
@@ -364,11 +371,13 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   __syncthreads();
 
   // ---------------- range phase: :203-205 for chirps w + 8 k2 --------------
-  const f4v* __restrict__ fr = reinterpret_cast<const f4v*>(a.iq + f * (int64_t)C * S);
-  const int S2 = S >> 1;                         // float4 (sample pairs) per chirp
+  // one load = one sample pair: 16 bytes (c64) or 8 bytes (c32h, half the L2 traffic)
+  using TP = std::conditional_t<H, h4v, f4v>;
+  const TP* __restrict__ fr = reinterpret_cast<const TP*>(a.iq) + f * (int64_t)C * (S >> 1);
+  const int S2 = S >> 1;                         // sample pairs per chirp
   const float ninvS = -1.0f / (float)S;
-  auto ld_chirp = [&](int k, f4v (&x)[8]) {
-    const f4v* __restrict__ q = fr + (int64_t)k * S2;
+  auto ld_chirp = [&](int k, TP (&x)[8]) {
+    const TP* __restrict__ q = fr + (int64_t)k * S2;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int p = lane + 64 * j;               // sample pair: samples 2p, 2p+1
@@ -379,7 +388,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   c2 tile0[CPW];                                 // slot 1 goes to LDS (L.t1)
   // chirp ring: the next chirp is in flight while one is consumed (a deeper
   // ring measured no faster: the VGPRs are worth more than the prefetch depth)
-  f4v buf[2][8];
+  TP buf[2][8];
   ld_chirp(w, buf[0]);
 #pragma unroll
   for (int k2 = 0; k2 < CPW; ++k2) {
@@ -388,7 +397,8 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     f4v x[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      x[j] = buf[k2 % 2][j];
+      if constexpr (H) x[j] = __builtin_convertvector(buf[k2 % 2][j], f4v);
+      else x[j] = buf[k2 % 2][j];
       if constexpr (!FULL)
         if (!(lane + 64 * j < S2)) x[j] = f4v{0.f, 0.f, 0.f, 0.f};
     }
@@ -549,7 +559,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
         // 16-byte stores: lane pairs (d2o even / odd) swap one value per d1s pair,
         // the even lane then writes elements (d2o, d2o + 1) of d1s = 2m, the odd
         // lane those of d1s = 2m + 1: 512 contiguous bytes per row and instruction
-        f4v* __restrict__ out = reinterpret_cast<f4v*>(a.rd + (f * NR + r) * (int64_t)ND);
+        TP* __restrict__ out = reinterpret_cast<TP*>(a.rd) + (f * NR + r) * (int64_t)(ND / 2);
         const bool odd = d2o & 1;
 #pragma unroll
         for (int m = 0; m < NW / 2; ++m) {
@@ -557,7 +567,9 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
           const c2 snd = odd ? A : B;
           const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
           const int e = (d2o & ~1) + CPW * (2 * m + (odd ? 1 : 0));
-          out[e >> 1] = odd ? f4v{rcv.x, rcv.y, B.x, B.y} : f4v{A.x, A.y, rcv.x, rcv.y};
+          const f4v o = odd ? f4v{rcv.x, rcv.y, B.x, B.y} : f4v{A.x, A.y, rcv.x, rcv.y};
+          if constexpr (H) out[e >> 1] = __builtin_convertvector(o * a.rd_scale, h4v);
+          else out[e >> 1] = o;
         }
         continue;
       }
@@ -600,9 +612,10 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeArgs a) {
   __shared__ float2 y[1024];
   __shared__ float2 red[16];
   const int tid = threadIdx.x, S = a.S, NR = a.NR;
-  const float2* __restrict__ x = a.iq + (a.frame * (int64_t)a.C + a.chirp) * S;
+  const int64_t x0 = (a.frame * (int64_t)a.C + a.chirp) * S;
+  auto x = [&](int n) { return op::ld_iq(a.iq, x0 + n, a.h); };
   float2 d = make_float2(0.f, 0.f);
-  for (int n = tid; n < S; n += 1024) d = cadd(d, make_float2(x[n].x - a.calw[n].x, x[n].y - a.calw[n].y));
+  for (int n = tid; n < S; n += 1024) d = cadd(d, make_float2(x(n).x - a.calw[n].x, x(n).y - a.calw[n].y));
   d = make_float2(op::wave_sum(d.x), op::wave_sum(d.y));
   if ((tid & 63) == 0) red[tid >> 6] = d;
   __syncthreads();
@@ -613,7 +626,7 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeArgs a) {
     float2 v = make_float2(0.f, 0.f);
     if (n < S) {
       const float4 c = a.calw[n];
-      v = cscale(make_float2(x[n].x - c.x - mu.x, x[n].y - c.y - mu.y), c.z);
+      v = cscale(make_float2(x(n).x - c.x - mu.x, x(n).y - c.y - mu.y), c.z);
     }
     y[n] = v;
   }
@@ -663,11 +676,11 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (j < n) {
-        const float2* __restrict__ row = a.rd + (f * NR + sel[j]) * (int64_t)a.ND;
+        const int64_t row = (f * NR + sel[j]) * (int64_t)a.ND;
         float bv = -1.f;
         int bi = INT_MAX;
         for (int e = lane; e < a.ND; e += 64) {
-          const float m = sqrtf(cabs2(row[e]));
+          const float m = sqrtf(cabs2(op::ld_iq(a.rd, row + e, a.rd_h))) * q.rd_unscale;
           if (m > bv) { bv = m; bi = e; }
         }
         wave_argmax(bv, bi);
@@ -707,18 +720,19 @@ __global__ __launch_bounds__(256) void k_slow_fix(SlowFixArgs a) {
     const int64_t f = a.fix_list[i];
     const int r = a.ridx[f * a.M] - 1;
     for (int k = w; k < C; k += 4) {
-      const float2* __restrict__ xc = a.iq + (f * C + k) * (int64_t)S;
+      const int64_t x0 = (f * C + k) * (int64_t)S;
+      auto xc = [&](int n) { return op::ld_iq(a.iq, x0 + n, a.h); };
       float2 s = make_float2(0.f, 0.f);
       for (int n = lane; n < S; n += 64) {
         const float4 c = a.calw[n];
-        s = cadd(s, make_float2(xc[n].x - c.x, xc[n].y - c.y));
+        s = cadd(s, make_float2(xc(n).x - c.x, xc(n).y - c.y));
       }
       s = make_float2(op::wave_sum(s.x), op::wave_sum(s.y));
       const float2 mu = cscale(s, 1.0f / (float)S);
       float2 acc = make_float2(0.f, 0.f);
       for (int n = lane; n < nmax; n += 64) {
         const float4 c = a.calw[n];
-        const float2 y = cscale(make_float2(xc[n].x - c.x - mu.x, xc[n].y - c.y - mu.y), c.z);
+        const float2 y = cscale(make_float2(xc(n).x - c.x - mu.x, xc(n).y - c.y - mu.y), c.z);
         const float2 tw = a.tw_nr[((int64_t)n * r) & (NR - 1)];
         acc = cadd(acc, cmul(y, tw));
       }
@@ -737,10 +751,13 @@ hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s) {
   if (a.F <= 0) return hipSuccess;
   if (!onepass_supported(a.S, a.C, op::NR, a.C)) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)(((a.F + 7) / 8) * 64);
-  if (a.S == op::NR)
-    hipLaunchKernelGGL((k_rd1p<true>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_rd1p<false>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+  if (a.S == op::NR) {
+    if (a.h) hipLaunchKernelGGL((k_rd1p<true, true>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+    else hipLaunchKernelGGL((k_rd1p<true, false>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+  } else {
+    if (a.h) hipLaunchKernelGGL((k_rd1p<false, true>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+    else hipLaunchKernelGGL((k_rd1p<false, false>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+  }
   return hipGetLastError();
 }
 

@@ -129,3 +129,68 @@ def test_onepass_rejects_unsupported(onepass):
     onepass.set_taps(cfg, cal, wr, wd)
     with pytest.raises(FmcwError, match="E_ARG"):
         onepass.process(iq)
+
+
+def _run_fp16(eng, iq16, F, C, want_rd=True):
+    import torch
+    from fmcw_radar_processing_amd import FMCW_C32H
+    d_iq = torch.from_numpy(iq16).cuda()
+    outs = dict(profile=torch.empty((F, 1024), device="cuda"),
+                tgt_count=torch.empty(F, dtype=torch.int32, device="cuda"),
+                tgt_range_idx=torch.empty((F, 1), dtype=torch.int32, device="cuda"),
+                tgt_range_mag=torch.empty((F, 1), device="cuda"),
+                tgt_doppler_idx=torch.empty((F, 1), dtype=torch.int32, device="cuda"),
+                slow_mag=torch.empty((F, C), device="cuda"))
+    d_rd = torch.empty((F, 1024, 256, 2), dtype=torch.float16, device="cuda") if want_rd else None
+    eng.process_device(d_iq, F, FMCW_C32H, outs, d_rd=d_rd, out_dtype=FMCW_C32H,
+                       stream=torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    got = {k: v.cpu().numpy() for k, v in outs.items()}
+    if want_rd:   # fp16 outputs hold D / (Nr*Nd) (include/fmcw.h, FMCW_C32H)
+        got["rd"] = d_rd.float().cpu().numpy().view(np.complex64)[..., 0].astype(np.complex128) * (1024 * 256)
+    return got
+
+
+# fp16 storage (BASELINE config 4 tolerance sweep): c32h IQ in, c32h RD out,
+# fp32 arithmetic, through the single pass.  SURVEY 8d: relative L2 <= 3e-3.
+@pytest.mark.parametrize("F,nts,fix", [(3, 1024, False), (21, 1024, False), (9, 1000, False), (10, 1024, True)])
+def test_onepass_fp16_storage(onepass, monkeypatch, F, nts, fix):
+    from tests.helpers import TOL_FP16_REL_L2
+    if fix:
+        monkeypatch.setenv("FMCW_ONEPASS_FORCE_FIX", "1")
+    cfg, p, wr, wd, cal, iq = _frames(F, nts, frame0=700)
+    onepass.set_taps(cfg, cal, wr, wd)
+    iq16 = np.stack([iq.real, iq.imag], -1).astype(np.float16)
+    got = _run_fp16(onepass, iq16, F, 256)
+    x = iq16.astype(np.float32).view(np.complex64)[..., 0]
+    ref = O.process_frames(x, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
+    assert rd_rel_err(got["rd"], ref["rd"], ref["cube"], wd, 256).max() <= TOL_FP16_REL_L2
+    # profile, slow row and detections come from fp32 values: the fp32 bars
+    assert rel_l2(got["profile"], ref["profile"], axis=1).max() <= TOL_FP32_REL_L2
+    ok = ~near_tie_frames(ref["profile"])
+    for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
+        np.testing.assert_array_equal(got[k][ok], ref[k][ok], err_msg=k)
+    has = ref["tgt_count"] > 0
+    assert has.sum() >= 1
+    assert rel_l2(got["slow_mag"][has], ref["slow_mag"][has], axis=1).max() <= TOL_FP32_REL_L2
+    assert np.all(got["slow_mag"][~has] == 0)
+
+
+def test_onepass_fp16_matches_streams_fp16(engine):
+    """AUTO picks the single pass for fp16 storage; it agrees with the streams
+    schedule's fp16 path within the fp16 bar, detections exactly."""
+    from tests.helpers import TOL_FP16_REL_L2
+    F = 16
+    cfg, p, wr, wd, cal, iq = _frames(F, frame0=1234)
+    engine.set_taps(cfg, cal, wr, wd)
+    iq16 = np.stack([iq.real, iq.imag], -1).astype(np.float16)
+    try:
+        engine.set_pipeline(FMCW_PIPE_AUTO, 0)
+        a = _run_fp16(engine, iq16, F, 256)
+        engine.set_pipeline(FMCW_PIPE_STREAMS)
+        b = _run_fp16(engine, iq16, F, 256)
+    finally:
+        engine.set_pipeline(FMCW_PIPE_AUTO, 0)
+    assert (rel_l2(a["rd"].reshape(F, -1), b["rd"].reshape(F, -1), axis=1) <= TOL_FP16_REL_L2).all()
+    for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
