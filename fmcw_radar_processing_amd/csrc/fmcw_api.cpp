@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -96,6 +97,7 @@ struct fmcw_ctx {
   DevBuf fused_ctrl, fused_slots, fused_rd_slots, fused_sticky;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
   DevBuf op_gh, op_tab;                        // single-pass tables (fmcw::OP_TAB_*)
+  DevBuf op_xbuf, op_xctl;                     // single pass, pair exchange: payload and flags/XCC ids (per chunk)
   float op_gh_scale = 0.f;                     // IF_scale op_gh was built for (0 = stale)
   bool fused_ran = false;
   int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
@@ -506,6 +508,8 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
       const double a = -2.0 * M_PI * (double)((i * d) & 255) / 256.0;
       put(fmcw::OP_TAB_TWR + i * 32 + d, std::cos(a), std::sin(a));
     }
+  for (int e = 0; e < 2; ++e)                 // pair range pass: W256^(2l + e) = W1024^(4 (2l + e))
+    for (int l = 0; l < 64; ++l) put(fmcw::OP_TAB_W256 + e * 64 + l, cr[(4 * (2 * l + e)) & (NR - 1)], ci[(4 * (2 * l + e)) & (NR - 1)]);
   for (int tt = 0; tt < 8; ++tt)
     for (int j = 0; j < 8; ++j)
       for (int e = 0; e < 2; ++e)
@@ -533,12 +537,20 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
                            int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
                            void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
   const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
-  const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : 8192);
+  // pair exchange (kernels_onepass.hip PAIR): default on; FMCW_ONEPASS_PAIR=0 selects the 8-tile range pass
+  bool pair = true;
+  if (const char* e = std::getenv("FMCW_ONEPASS_PAIR"); e && e[0] == '0') pair = false;
+  // the exchange payload is 1 MiB per frame of a chunk: chunks of at most 1024 frames
+  const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : (pair ? 1024 : 8192));
   constexpr int TC = fmcw::OP_TILES * fmcw::OP_CAND;
   CHK(c->op_rowpk.ensure((size_t)chunk * NR * 8));
   CHK(c->op_cidx.ensure((size_t)chunk * TC * 4));
   CHK(c->op_crows.ensure((size_t)chunk * TC * C * 4));
   CHK(c->op_fix.ensure((size_t)chunk * 4 + 16));
+  if (pair) {
+    CHK(c->op_xbuf.ensure((size_t)chunk * 8 * 8 * 16 * 64 * 16));
+    CHK(c->op_xctl.ensure((size_t)chunk * 8 * 4 * 2));
+  }
   int32_t* fix_count = c->op_fix.as<int32_t>();
   int32_t* fix_list = fix_count + 4;
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
@@ -573,11 +585,57 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;
     }
+    if (pair) {
+      a.pair = 1;
+      a.xbuf = c->op_xbuf.as<float4>();
+      a.xflag = c->op_xctl.as<unsigned>();
+      a.xcc = a.xflag + nf * 8;
+      if (const char* e = std::getenv("FMCW_ONEPASS_XMODE")) a.xmode = std::atoi(e);
+      HIPCHK(hipMemsetAsync(a.xflag, 0xFF, (size_t)nf * 8 * 4 * 2, s));   // flags and XCC ids: "not yet"
+    }
+#ifdef OP_STAMPS
+    static unsigned long long* dbg = nullptr;
+    const size_t nblk = (size_t)((nf + 7) / 8) * 64;
+    if (!dbg) HIPCHK(hipMalloc(&dbg, (size_t)1 << 24));
+    a.dbg = dbg;
+#endif
     {
       StageTimer tm(c, 8, s, 2);
       HIPCHK(fmcw::launch_onepass(a, s));
       tm.done();
     }
+#ifdef OP_STAMPS
+    {   // diagnostic build: per-phase durations and concurrency of k_rd1p (100 MHz realtime clock)
+      // stamps: 0 entry, 1 prologue issued, 2 wave 0 range loop done, 3 reductions done,
+      //         4 Doppler stores issued, 5 stores drained
+      std::vector<unsigned long long> h(nblk * 8);
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
+      unsigned long long lo = ~0ull, hi = 0;
+      double ph[5] = {0, 0, 0, 0, 0};
+      for (size_t i = 0; i < nblk; ++i) {
+        lo = std::min(lo, h[8 * i]); hi = std::max(hi, h[8 * i + 5]);
+        for (int q = 0; q < 5; ++q) ph[q] += (double)(h[8 * i + q + 1] - h[8 * i + q]);
+      }
+      const double span = (double)(hi - lo);
+      double life = 0;
+      for (int q = 0; q < 5; ++q) life += ph[q];
+      std::fprintf(stderr, "stamps: blocks %zu span %.1f us | per block us: prologue %.2f range %.2f reduce %.2f "
+                   "doppler %.2f drain %.2f (life %.2f) | avg resident %.1f\n", nblk, span / 100.0,
+                   ph[0] / nblk / 100.0, ph[1] / nblk / 100.0, ph[2] / nblk / 100.0, ph[3] / nblk / 100.0,
+                   ph[4] / nblk / 100.0, life / nblk / 100.0, life / span);
+      if (a.pair) {   // 6: own half done (wave 0), 7: hand-off flag seen
+        double q[3] = {0, 0, 0};
+        for (size_t i = 0; i < nblk; ++i) {
+          q[0] += (double)(h[8 * i + 6] - h[8 * i + 1]);
+          q[1] += (double)(h[8 * i + 7] - h[8 * i + 6]);
+          q[2] += (double)(h[8 * i + 2] - h[8 * i + 7]);
+        }
+        std::fprintf(stderr, "stamps pair: own half %.2f  publish+wait %.2f  receive %.2f us per block\n",
+                     q[0] / nblk / 100.0, q[1] / nblk / 100.0, q[2] / nblk / 100.0);
+      }
+    }
+#endif
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
     fmcw::Detect1pArgs k{};
     k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.rd_h = h; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
@@ -806,6 +864,10 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
   if (pn < 1 || n_halo < 0 || max_seg < 0 || !(fs > 0)) return fail(FMCW_E_ARG, "bad pn / n_halo / max_seg / fs");
   if (!d_slow || !d_list || !d_len || !d_win || !d_P || !d_pmax || !d_nseg || (n_halo > 0 && !d_halo))
     return fail(FMCW_E_ARG, "NULL device pointer");
+  // the shard split of the slow-time signal (dist.py) starts every shard's segment grid at its own
+  // sample 0 and takes wlen-1 samples of right halo: that is the global grid only for hop 1
+  if (n_halo > 0 && wlen - noverlap != 1)
+    return fail(FMCW_E_ARG, "a halo (sharded STFT) needs hop 1, i.e. noverlap = wlen - 1");
   CHK(set_device(c));
   hipStream_t s = pick(c, stream);
   fmcw::StftArgs a{};

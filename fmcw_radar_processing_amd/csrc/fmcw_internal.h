@@ -107,7 +107,8 @@ constexpr int OP_CAND = 2;           // slow-time candidate rows kept per tile
 constexpr int OP_TAB_LANE = 0;       // [6][64]: DIF twiddles of spans 32..2 (1 on clear lanes of spans 8..2), W128^lane_bin(l)
 constexpr int OP_TAB_TWR = 384;      // [8][32]: W256^(i d2)
 constexpr int OP_TAB_CST = 640;      // [8 t][8 j][2 e][64 l]: w'[n] W1024^(t n), n = 2l + e + 128j
-constexpr int OP_TAB_SIZE = 640 + 8 * 1024;
+constexpr int OP_TAB_W256 = 640 + 8 * 1024;   // [2 e][64 l]: W256^(2l + e) (pair range pass)
+constexpr int OP_TAB_SIZE = OP_TAB_W256 + 128;
 
 struct OnePassArgs {
   const void* iq;          // [F][C][S] c64, or c32h when h
@@ -130,6 +131,13 @@ struct OnePassArgs {
   float range_thr, min_d, max_d, dist_per_bin;
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
+  unsigned long long* dbg; // diagnostic builds only (-DOP_STAMPS): [blocks][8] s_memrealtime stamps
+  int pair;                // pair-exchange range pass (kernels_onepass.hip, PAIR)
+  float4* xbuf;            // pair: [F][8 t][8 w][16 i][64 l] {slot0, slot1} of tile t ^ 4, from tile t's chirps
+  unsigned* xflag;         // pair: [F][8] hand-off flags (1 = same-XCD publish, 2 = released), 0xFFFFFFFF before
+  unsigned* xcc;           // pair: [F][8] XCC_ID of each tile's workgroup, 0xFFFFFFFF before
+  int xmode;               // pair test knob (FMCW_ONEPASS_XMODE): 0 normal, 1 always release the
+                           // hand-off, 2 never take the partner's half (recompute it locally)
 };
 
 struct Detect1pArgs {

@@ -317,21 +317,47 @@ __device__ __forceinline__ void dft32p(c2 (&v)[32]) {
 // LDS image of k_rd1p.
 struct Lds1p {
   c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the corner turn
-  f4v gh0[64], gh1[64];    // {Gh, Hh} of lane l's bins r0(l), r1(l) (lane order: conflict-free reads)
+  f4v gh[4][64];           // {Gh, Hh} of lane l's bins (lane order: conflict-free reads):
+                           //   single tile: [0] r0(l), [1] r1(l) of tile t
+                           //   pair:        [0], [1] of tile p, [2], [3] of tile p + 4
   float red[2][NW][3][64]; // per-wave {sum.re, sum.im, max |X|^2} of each row over the wave's chirps
   float cand[OP_CAND][256];// candidate rows |X|^2 as [wave][k2] (chirp w + 8 k2), written out coalesced
+  int xok;                 // pair: the partner's half arrived (else it is recomputed here)
 };
+
+constexpr int XTMO = 20000;    // pair: bounded wait for the partner, s_memrealtime ticks (100 MHz): 200 us
 
 }  // namespace op
 
 // ---------------------------------------------------------------------------
 // k_rd1p: one workgroup (8 waves, 2 per SIMD, 256 VGPRs per lane) = one range
 // tile of one frame.  FULL: S == NR (no zero padding, no masking).
+//
+// PAIR (the default for complex64 / fp16 at NR 1024, PN 256): the range pass
+// of tile t = p + 4h (p < 4, h < 2) covers only chirp half h, but computes the
+// 256 bins r == p (mod 4) of each of its chirps -- its own tile's 128 bins
+// (r == t mod 8) and those of its partner tile t ^ 4.  The partner's bins go
+// to the partner workgroup through the XCD's L2 (128 KiB each way), so every
+// sample is read by 4 workgroups instead of 8 and stage A runs once per
+// (sample, p) instead of once per (sample, t):
+//   n = a + 256 b (a < 256, b < 4), r = p + 4 m:
+//   X[p + 4m] = sum_a W256^(a m) A[a],   A[a] = sum_b y[a + 256 b] W1024^(p (a + 256 b))
+//   a = a' + 128 q:  even m = 2m': 128-point FFT of A[a'] + A[a' + 128]            -> tile p
+//                    odd  m:      128-point FFT of (A[a'] - A[a' + 128]) W256^a'    -> tile p + 4
+// Hand-off (placement-independent, MI355X_MICROARCH.md visibility rules): plain
+// 16-byte stores, every wave drains (vmcnt 0), barrier, then one lane raises
+// the workgroup's flag with an agent-scope store -- after an agent release
+// fence unless the partner has announced the same XCC_ID (then the bytes are
+// already in the one L2 both read).  The consumer polls the partner's flag
+// (relaxed agent load, bounded) and reads the bytes with sc1 loads (past its
+// L1).  A partner that does not arrive within XTMO is not waited for: its half
+// is recomputed locally (same arithmetic), so no schedule can deadlock.
 // ---------------------------------------------------------------------------
-template <bool FULL, bool H>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
+template <bool FULL, bool H, bool PAIR>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
 __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   using namespace op;
   constexpr int CPW = 32, C = NW * CPW, ND = C;  // wave w owns chirps w + 8 k2, k2 < 32
+  constexpr int HPW = CPW / 2;                   // pair: chirps per wave in one half
   __shared__ __attribute__((aligned(16))) Lds1p L;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -341,22 +367,32 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   const int t = (b >> 3) & 7;
   if (f >= a.F) return;                          // block-uniform
   const int S = FULL ? NR : a.S;
+#ifdef OP_STAMPS
+  if (tid == 0) a.dbg[(int64_t)b * 8] = __builtin_amdgcn_s_memrealtime();
+#endif
+  const int p4 = t & 3, h = t >> 2, tq = t ^ 4;  // pair: bins r == p4 (mod 4), chirp half h, partner tile
+  unsigned xcc = 0;
+  if constexpr (PAIR) {
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (tid == 0) __hip_atomic_store(a.xcc + f * 8 + t, xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
   // Per-tile tables come from host-built arrays laid out in lane order
   // (fmcw_api.cpp build_onepass_gh), so every table read is a coalesced
   // 512-byte wave access: gathers here would cost the L2 as many requests as
   // the frame itself.
   const c2* __restrict__ tab = reinterpret_cast<const c2*>(a.tab);
-  if (tid < 128) (tid < 64 ? L.gh0 : L.gh1)[lane] = reinterpret_cast<const f4v*>(a.gh)[(2 * t + (tid >> 6)) * 64 + lane];
-  // stage-A constants c_t[n] = w'[n] W1024^(t n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
+  {
+    const int tg = PAIR ? p4 + 4 * (tid >> 7) : t;           // pair: tiles p4 and p4 + 4
+    if (tid < (PAIR ? 256 : 128)) L.gh[tid >> 6][lane] = reinterpret_cast<const f4v*>(a.gh)[(2 * tg + ((tid >> 6) & 1)) * 64 + lane];
+  }
+  // stage-A constants c_ts[n] = w'[n] W1024^(ts n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
+  const int ts = PAIR ? p4 : t;
   c2 cst[16];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) cst[2 * j + e] = tab[OP_TAB_CST + ((t * 8 + j) * 2 + e) * 64 + lane];
-  c2 cs7[2];                                     // rotated copies for the last, compiler-visible MAC
-  cs7[0] = c2{-cst[14].y, cst[14].x};
-  cs7[1] = c2{-cst[15].y, cst[15].x};
+    for (int e = 0; e < 2; ++e) cst[2 * j + e] = tab[OP_TAB_CST + ((ts * 8 + j) * 2 + e) * 64 + lane];
   c2 twh[5];                                     // spans 32, 16 (every lane), 8, 4, 2 (1 on clear lanes)
   float sg[6];                                   // spans 32 .. 1
 #pragma unroll
@@ -368,6 +404,12 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   const int m0 = lane_bin(lane);
   const c2 w128 = tab[OP_TAB_LANE + 5 * 64 + lane];
   const int r0 = t + 8 * m0, r1 = r0 + 512;      // this lane's two range bins
+#ifdef OP_STAMPS
+  auto stamp = [&](int i) { if (tid == 0) a.dbg[(int64_t)b * 8 + i] = __builtin_amdgcn_s_memrealtime(); };
+#else
+  auto stamp = [](int) {};
+#endif
+  stamp(1);
   __syncthreads();
 
   // ---------------- range phase: :203-205 for chirps w + 8 k2 --------------
@@ -385,53 +427,166 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       else x[j] = q[p < S2 ? p : 0];
     }
   };
-  c2 tile0[CPW];                                 // slot 1 goes to LDS (L.t1)
-  // chirp ring: the next chirp is in flight while one is consumed (a deeper
-  // ring measured no faster: the VGPRs are worth more than the prefetch depth)
-  TP buf[2][8];
-  ld_chirp(w, buf[0]);
-#pragma unroll
-  for (int k2 = 0; k2 < CPW; ++k2) {
-    const int k = w + NW * k2;
-    if (k2 + 1 < CPW) ld_chirp(k + NW, buf[(k2 + 1) % 2]);
-    f4v x[8];
+  auto widen = [&](const TP (&bf)[8], f4v (&x)[8]) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      if constexpr (H) x[j] = __builtin_convertvector(buf[k2 % 2][j], f4v);
-      else x[j] = buf[k2 % 2][j];
+      if constexpr (H) x[j] = __builtin_convertvector(bf[j], f4v);
+      else x[j] = bf[j];
       if constexpr (!FULL)
         if (!(lane + 64 * j < S2)) x[j] = f4v{0.f, 0.f, 0.f, 0.f};
     }
-    // stage A: sum_b x[a + 128 b] c_t[a + 128 b], straight from the loads
-    c2 A0 = cmul_a(x[0].xy, cst[0]), A1 = cmul_a(x[0].zw, cst[1]);
-    f4v s4 = x[0];
+  };
+  // 128-point FFT across lanes of (R0, R1) = (a' = 2 lane, 2 lane + 1):
+  // spans 32, 16 as pair butterflies, then four 16-point DIFs per register
+  auto fft128 = [&](c2& R0, c2& R1) {
+    pair_bfly<32>(R0, R1, twh[0]);
+    pair_bfly<16>(R0, R1, twh[1]);
+    R0 = dif_stage<8>(R0, twh[2], sg[2]);  R1 = dif_stage<8>(R1, twh[2], sg[2]);
+    R0 = dif_stage<4>(R0, twh[3], sg[3]);  R1 = dif_stage<4>(R1, twh[3], sg[3]);
+    R0 = dif_stage<2>(R0, twh[4], sg[4]);  R1 = dif_stage<2>(R1, twh[4], sg[4]);
+    R0 = dif_stage<1>(R0, twh[4], sg[5]);  R1 = dif_stage<1>(R1, twh[4], sg[5]);
+    pair_swap32(R0, R1);                          // lane l: E[m], O[m], m = lane_bin(l)
+  };
+  // :204 the chirp mean, applied to the spectrum: X -= Gh + mean(x) Hh
+  auto finish = [&](c2 R0, c2 R1, c2 nmx, f4v g0, f4v g1, c2& X0, c2& X1) {
+    const c2 ow = cmv(R1, w128);
+    X0 = cmac_a(R0 + ow - g0.xy, nmx, g0.zw);    // bin r0 (slot 0)
+    X1 = cmac_a(R0 - ow - g1.xy, nmx, g1.zw);    // bin r1 (slot 1)
+  };
+#ifndef OP_RING
+#define OP_RING 2
+#endif
+  constexpr int RING = OP_RING;                  // chirps in registers: RING - 1 in flight while one is consumed
+  c2 tile0[CPW];                                 // slot 1 goes to LDS (L.t1)
+
+  if constexpr (!PAIR) {
+    c2 cs7[2];                                   // rotated copies for the last, compiler-visible MAC
+    cs7[0] = c2{-cst[14].y, cst[14].x};
+    cs7[1] = c2{-cst[15].y, cst[15].x};
+    TP buf[RING][8];
 #pragma unroll
-    for (int j = 1; j < 7; ++j) {
-      A0 = cmac_a(A0, x[j].xy, cst[2 * j]);
-      A1 = cmac_a(A1, x[j].zw, cst[2 * j + 1]);
-      s4 += x[j];
+    for (int i = 0; i < RING - 1; ++i) ld_chirp(w + NW * i, buf[i]);
+#pragma unroll
+    for (int k2 = 0; k2 < CPW; ++k2) {
+      const int k = w + NW * k2;
+      if (k2 + RING - 1 < CPW) ld_chirp(k + NW * (RING - 1), buf[(k2 + RING - 1) % RING]);
+      f4v x[8];
+      widen(buf[k2 % RING], x);
+      // stage A: sum_b x[a + 128 b] c_t[a + 128 b], straight from the loads
+      c2 A0 = cmul_a(x[0].xy, cst[0]), A1 = cmul_a(x[0].zw, cst[1]);
+      f4v s4 = x[0];
+#pragma unroll
+      for (int j = 1; j < 7; ++j) {
+        A0 = cmac_a(A0, x[j].xy, cst[2 * j]);
+        A1 = cmac_a(A1, x[j].zw, cst[2 * j + 1]);
+        s4 += x[j];
+      }
+      A0 = cmacv(A0, x[7].xy, cst[14], cs7[0]);   // compiler-visible producer for the DPP stages
+      A1 = cmacv(A1, x[7].zw, cst[15], cs7[1]);
+      s4 += x[7];
+      fft128(A0, A1);
+      const c2 nmx = wave_sum_c(s4.xy + s4.zw) * ninvS;
+      c2 X0, X1;
+      finish(A0, A1, nmx, L.gh[0][lane], L.gh[1][lane], X0, X1);
+      tile0[k2] = X0;
+      L.t1[k * 64 + lane] = X1;
     }
-    A0 = cmacv(A0, x[7].xy, cst[14], cs7[0]);   // compiler-visible producer for the DPP stages
-    A1 = cmacv(A1, x[7].zw, cst[15], cs7[1]);
-    s4 += x[7];
-    pair_bfly<32>(A0, A1, twh[0]);                // E = DFT64(A0), O = DFT64(A1): spans 32, 16 as pair
-    pair_bfly<16>(A0, A1, twh[1]);                // butterflies, then four 16-point DIFs per register
-    A0 = dif_stage<8>(A0, twh[2], sg[2]);  A1 = dif_stage<8>(A1, twh[2], sg[2]);
-    A0 = dif_stage<4>(A0, twh[3], sg[3]);  A1 = dif_stage<4>(A1, twh[3], sg[3]);
-    A0 = dif_stage<2>(A0, twh[4], sg[4]);  A1 = dif_stage<2>(A1, twh[4], sg[4]);
-    A0 = dif_stage<1>(A0, twh[4], sg[5]);  A1 = dif_stage<1>(A1, twh[4], sg[5]);
-    pair_swap32(A0, A1);                          // lane l: E[m], O[m], m = lane_bin(l)
-    // :204 the chirp mean, applied to the spectrum: X -= Gh + mean(x) Hh
-    const c2 nmx = wave_sum_c(s4.xy + s4.zw) * ninvS;
-    const f4v g0 = L.gh0[lane], g1 = L.gh1[lane];
-    const c2 ow = cmv(A1, w128);
-    const c2 X0 = cmac_a(A0 + ow - g0.xy, nmx, g0.zw);   // bin r0 of chirp k
-    const c2 X1 = cmac_a(A0 - ow - g1.xy, nmx, g1.zw);   // bin r1
-    tile0[k2] = X0;
-    L.t1[k * 64 + lane] = X1;
+  } else {
+    const c2 w256a = tab[OP_TAB_W256 + lane], w256b = tab[OP_TAB_W256 + 64 + lane];   // W256^(2 lane + e)
+    // range pass over chirp half hh: own tile's bins -> own[] (slot 0) and L.t1 (slot 1);
+    // the partner tile's bins -> the exchange buffer when xs
+    f4v* __restrict__ xout = reinterpret_cast<f4v*>(a.xbuf) + ((f * 8 + t) * NW + w) * (int64_t)(HPW * 64) + lane;
+    auto range_half = [&](int hh, c2 (&own)[HPW], bool xs) {
+      const int kb = w + NW * HPW * hh;           // chirp of step i: kb + NW i
+      TP buf[RING][8];
+#pragma unroll
+      for (int i = 0; i < RING - 1; ++i) ld_chirp(kb + NW * i, buf[i]);
+#pragma unroll
+      for (int i = 0; i < HPW; ++i) {
+        const int k = kb + NW * i;
+        if (i + RING - 1 < HPW) ld_chirp(k + NW * (RING - 1), buf[(i + RING - 1) % RING]);
+        f4v x[8];
+        widen(buf[i % RING], x);
+        // stage A: A[a' + 128 q] = sum_b x[a' + 128 q + 256 b] c_p[.], q = j & 1, b = j >> 1
+        c2 A00 = cmul_a(x[0].xy, cst[0]), A10 = cmul_a(x[0].zw, cst[1]);
+        c2 A01 = cmul_a(x[1].xy, cst[2]), A11 = cmul_a(x[1].zw, cst[3]);
+        f4v s4 = x[0] + x[1];
+#pragma unroll
+        for (int j = 2; j < 8; j += 2) {
+          A00 = cmac_a(A00, x[j].xy, cst[2 * j]);
+          A10 = cmac_a(A10, x[j].zw, cst[2 * j + 1]);
+          A01 = cmac_a(A01, x[j + 1].xy, cst[2 * j + 2]);
+          A11 = cmac_a(A11, x[j + 1].zw, cst[2 * j + 3]);
+          s4 += x[j] + x[j + 1];
+        }
+        // radix 2 over q (compiler-visible producers for the DPP stages)
+        c2 E0 = A00 + A01, E1 = A10 + A11;                   // even m: tile p
+        c2 O0 = cmv(A00 - A01, w256a), O1 = cmv(A10 - A11, w256b);   // odd m: tile p + 4
+        fft128(E0, E1);
+        fft128(O0, O1);
+        const c2 nmx = wave_sum_c(s4.xy + s4.zw) * ninvS;
+        c2 XE0, XE1, XO0, XO1;
+        finish(E0, E1, nmx, L.gh[0][lane], L.gh[1][lane], XE0, XE1);
+        finish(O0, O1, nmx, L.gh[2][lane], L.gh[3][lane], XO0, XO1);
+        own[i] = h ? XO0 : XE0;
+        L.t1[k * 64 + lane] = h ? XO1 : XE1;
+        if (xs) {
+          const c2 y0 = h ? XE0 : XO0, y1 = h ? XE1 : XO1;
+          xout[i * 64] = f4v{y0.x, y0.y, y1.x, y1.y};
+        }
+      }
+    };
+    c2 own[HPW], rcv[HPW];
+    range_half(h, own, true);
+    stamp(6);
+    // hand-off: publish this half of the partner's tile, then take the partner's half of ours
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave drains its stores
+    __syncthreads();
+    if (tid == 0) {
+      unsigned v = 1;
+      if (a.xmode == 1 || __hip_atomic_load(a.xcc + f * 8 + tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != xcc) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // partner elsewhere (or not started): write back L2
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        v = 2;
+      }
+      __hip_atomic_store(a.xflag + f * 8 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int ok = 0;
+      for (; a.xmode != 2;) {                      // xmode 2 (test knob): never take the partner's half
+        const unsigned q = __hip_atomic_load(a.xflag + f * 8 + tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (q == 1u || q == 2u) { ok = 1; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)XTMO) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      L.xok = ok;
+    }
+    __syncthreads();
+    stamp(7);
+    const int kq = w + NW * HPW * (1 - h);         // partner half: chirps kq + NW i
+    if (__builtin_amdgcn_readfirstlane(L.xok)) {
+      const f4v* src = reinterpret_cast<const f4v*>(a.xbuf) + ((f * 8 + tq) * NW + w) * (int64_t)(HPW * 64) + lane;
+      f4v v[HPW];
+#pragma unroll
+      for (int i = 0; i < HPW; ++i)                 // sc1: past this CU's L1 (never a stale copy)
+        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[i]) : "v"(src + i * 64) : "memory");
+      asm volatile("s_waitcnt vmcnt(0)"
+                   : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+                     "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+                   :: "memory");
+#pragma unroll
+      for (int i = 0; i < HPW; ++i) {
+        rcv[i] = c2{v[i].x, v[i].y};
+        L.t1[(kq + NW * i) * 64 + lane] = c2{v[i].z, v[i].w};
+      }
+    } else {
+      range_half(1 - h, rcv, false);              // partner absent: the same arithmetic here
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < CPW; ++k2) tile0[k2] = ((k2 < HPW) == (h == 0)) ? own[k2 % HPW] : rcv[k2 % HPW];
   }
 
   // ---------------- per-row reductions over the 8 waves --------------------
+  stamp(2);
   __syncthreads();                               // B1: slot 1 complete in LDS
   c2 tile1[CPW];
 #pragma unroll
@@ -464,6 +619,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   mu0 *= 1.0f / (float)C;                        // :217 mean over all chirps
   mu1 *= 1.0f / (float)C;
   const float pr0 = sqrtf(q0), pr1 = sqrtf(q1);  // :210 / :265 abs(max(X,[],2))
+  stamp(3);
   if (w == 0) {
     a.profile[f * NR + r0] = pr0;
     a.profile[f * NR + r1] = pr1;
@@ -602,6 +758,11 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   stage(tile1);
   __syncthreads();                               // B5
   post(1);
+  stamp(4);
+#ifdef OP_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  stamp(5);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -750,14 +911,19 @@ bool onepass_supported(int nts, int pn, int nr, int nd) {
 hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s) {
   if (a.F <= 0) return hipSuccess;
   if (!onepass_supported(a.S, a.C, op::NR, a.C)) return hipErrorInvalidValue;
+  if (a.pair && (!a.xbuf || !a.xflag || !a.xcc)) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)(((a.F + 7) / 8) * 64);
-  if (a.S == op::NR) {
-    if (a.h) hipLaunchKernelGGL((k_rd1p<true, true>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
-    else hipLaunchKernelGGL((k_rd1p<true, false>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+  const dim3 g(blocks), bl(64 * op::NW);
+#define FMCW_OP_LAUNCH(FU, HH, PP) hipLaunchKernelGGL((k_rd1p<FU, HH, PP>), g, bl, 0, s, a)
+  const bool full = a.S == op::NR;
+  if (a.pair) {
+    if (full) { if (a.h) FMCW_OP_LAUNCH(true, true, true); else FMCW_OP_LAUNCH(true, false, true); }
+    else { if (a.h) FMCW_OP_LAUNCH(false, true, true); else FMCW_OP_LAUNCH(false, false, true); }
   } else {
-    if (a.h) hipLaunchKernelGGL((k_rd1p<false, true>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
-    else hipLaunchKernelGGL((k_rd1p<false, false>), dim3(blocks), dim3(64 * op::NW), 0, s, a);
+    if (full) { if (a.h) FMCW_OP_LAUNCH(true, true, false); else FMCW_OP_LAUNCH(true, false, false); }
+    else { if (a.h) FMCW_OP_LAUNCH(false, true, false); else FMCW_OP_LAUNCH(false, false, false); }
   }
+#undef FMCW_OP_LAUNCH
   return hipGetLastError();
 }
 

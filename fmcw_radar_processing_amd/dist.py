@@ -40,6 +40,8 @@ def all_lengths(L_local: torch.Tensor) -> torch.Tensor:
 def head_samples(slow_mag: torch.Tensor, frame_list: torch.Tensor, L_local: torch.Tensor, h: int) -> torch.Tensor:
     """First h samples of this rank's compacted signal (zeros past L), on device, no host sync."""
     pn = slow_mag.shape[1]
+    if frame_list.numel() == 0 or slow_mag.shape[0] == 0:       # empty shard (F_total < world)
+        return torch.zeros(h, dtype=slow_mag.dtype, device=slow_mag.device)
     q = torch.arange(h, device=slow_mag.device)
     fi = torch.clamp(q // pn, max=frame_list.numel() - 1)
     fr = frame_list[fi].long().clamp(0, slow_mag.shape[0] - 1)

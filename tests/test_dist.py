@@ -30,7 +30,8 @@ def _free_port():
 def _scenario(F, C, seed):
     g = np.random.default_rng(seed)
     count = (g.random(F) > 0.3).astype(np.int32)
-    count[F // 3: F // 3 + 4] = 0            # a run of empty frames (a shard may see none)
+    if F > 4:
+        count[F // 3: F // 3 + 4] = 0        # a run of empty frames (a shard may see none)
     slow = np.abs(g.standard_normal((F, C))) * count[:, None]
     ridx = (g.integers(5, 100, F) * count).astype(np.int32)[:, None]
     didx = (g.integers(1, 17, F) * count).astype(np.int32)[:, None]
@@ -75,7 +76,8 @@ def _worker(rank, world, port, F, C, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,F,C", [(2, 13, 8), (3, 12, 4), (4, 17, 4)])
+@pytest.mark.parametrize("world,F,C", [(2, 13, 8), (3, 12, 4), (4, 17, 4),
+                                        (4, 3, 32)])   # F < world: rank 3 owns no frame at all
 def test_sharded_stft_equals_single_process(world, F, C):
     from oracle import oracle as O
     ctx = mp.get_context("spawn")
