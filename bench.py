@@ -39,9 +39,8 @@ def parse():
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU per step")
     ap.add_argument("--fp16", action="store_true", help="config-4 fp16 storage variant")
     ap.add_argument("--chunk", type=int, default=0, help="frames per range/Doppler chunk (0 = library default)")
-    ap.add_argument("--pipeline", choices=["auto", "streams", "fused", "onepass"], default="auto",
+    ap.add_argument("--pipeline", choices=["auto", "streams", "onepass"], default="auto",
                     help="range/Doppler schedule (include/fmcw.h fmcw_set_pipeline)")
-    ap.add_argument("--nslot", type=int, default=0, help="fused schedule: cube slots per XCD (0 = default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--no-fanout", action="store_true")
@@ -75,7 +74,7 @@ def main():
     eng.set_taps(cfg, P.synth_calibration(S))
     if args.chunk:
         eng.set_chunk_frames(args.chunk)
-    eng.set_pipeline({"auto": 0, "streams": 1, "fused": 2, "onepass": 3}[args.pipeline], args.nslot)
+    eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3}[args.pipeline])
     stream = torch.cuda.current_stream(dev)
 
     # ---- device-resident input + outputs ------------------------------------------
@@ -141,8 +140,6 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     stages = eng.timing_read() if level else {}
-    if eng.pipeline_status() != 0:
-        raise RuntimeError("fused schedule reported a bounded-wait timeout: results invalid")
     eng.timing(0)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
@@ -200,10 +197,6 @@ def main():
                 "alg_bytes_per_launch": k["alg_bytes_per_launch"], "avg_launch_us": k["avg_launch_us"],
                 "frames_per_launch": k["frames_per_launch"],
                 "traffic_source": pmc.get("source") if pmc and traffic else None}
-    elif path:
-        roof = {"bound": "hbm", "achieved": path["achieved"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                "frac": path["frac"], "traffic": None, "kernel": "k_rd_fused (one launch per step)",
-                "avg_launch_us": path["span_us"], "frames_per_launch": path["frames_per_span"]}
 
     # ---- input fan-out over xGMI from rank 0 (reported separately, not in value) -----
     fanout = None

@@ -16,7 +16,8 @@ LIB_PATH = os.environ.get("FMCW_LIB", os.path.join(_HERE, "libfmcw.so"))
 FMCW_OK = 0
 FMCW_E_ARG, FMCW_E_HIP, FMCW_E_OOM, FMCW_E_STATE, FMCW_E_DATA = -1, -2, -3, -4, -5
 FMCW_C64, FMCW_C32H = 0, 1
-FMCW_PIPE_AUTO, FMCW_PIPE_STREAMS, FMCW_PIPE_FUSED, FMCW_PIPE_ONEPASS = 0, 1, 2, 3
+FMCW_PIPE_AUTO, FMCW_PIPE_STREAMS, FMCW_PIPE_ONEPASS = 0, 1, 3
+ABI_VERSION = 2
 STATUS_NAMES = {0: "OK", -1: "E_ARG", -2: "E_HIP", -3: "E_OOM", -4: "E_STATE", -5: "E_DATA"}
 STAGES = ("range", "doppler", "detect", "compact", "stft_power", "stft_db", "range_only", "range_doppler", "onepass")
 
@@ -46,8 +47,9 @@ SIGNATURES = {
     "fmcw_abi_version": (_I32, []),
     "fmcw_last_error": (ct.c_char_p, []),
     "fmcw_device_count": (ct.c_int, [ct.POINTER(_I32)]),
-    "fmcw_ctx_create": (ct.c_int, [_I32, ct.POINTER(_P)]),
+    "fmcw_ctx_create": (ct.c_int, [_I32, ct.POINTER(_I32), ct.POINTER(_P)]),
     "fmcw_ctx_destroy": (ct.c_int, [_P]),
+    "fmcw_ctx_devices": (ct.c_int, [_P, ct.POINTER(_I32), ct.POINTER(_I32), ct.POINTER(_I32)]),
     "fmcw_set_taps": (ct.c_int, [_P, _PP, _P, _P, _P]),
     "fmcw_process": (ct.c_int, [_P, _PP, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _I64, _P]),
     "fmcw_range_fft": (ct.c_int, [_P, _PP, _P, _I32, _I64, _P, _P]),
@@ -66,8 +68,7 @@ SIGNATURES = {
     "fmcw_timing_read": (ct.c_int, [_P, _I32, ct.POINTER(_D), ct.POINTER(_I64)]),
     "fmcw_timing_reset": (ct.c_int, [_P]),
     "fmcw_set_chunk_frames": (ct.c_int, [_P, _I64]),
-    "fmcw_set_pipeline": (ct.c_int, [_P, _I32, _I32]),
-    "fmcw_pipeline_status": (ct.c_int, [_P, ct.POINTER(_I32)]),
+    "fmcw_set_pipeline": (ct.c_int, [_P, _I32]),
     "fmcw_synchronize": (ct.c_int, [_P]),
 }
 
@@ -94,7 +95,7 @@ def load() -> ct.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fmcw_abi_version() != 1:
+    if lib.fmcw_abi_version() != ABI_VERSION:
         raise FmcwError(FMCW_E_STATE, "libfmcw ABI version mismatch")
     _lib = lib
     return lib

@@ -8,7 +8,9 @@
 #include "../../include/fmcw.h"
 #include "fmcw_internal.h"
 
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -16,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -69,6 +72,54 @@ struct DevBuf {
 
 size_t esize(int dtype) { return dtype == FMCW_C32H ? 4 : 8; }
 
+// RCCL, resolved at run time: a single-device context never needs it, and a
+// process that already holds an RCCL (torch's) shares that copy.
+struct Rccl {
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+  bool ok = false;
+};
+
+const Rccl& rccl() {
+  static Rccl r = [] {
+    Rccl x;
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+      h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
+      if (h) break;
+    }
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return x;
+    x.comm_init_all = reinterpret_cast<decltype(x.comm_init_all)>(dlsym(h, "ncclCommInitAll"));
+    x.comm_destroy = reinterpret_cast<decltype(x.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+    x.all_reduce = reinterpret_cast<decltype(x.all_reduce)>(dlsym(h, "ncclAllReduce"));
+    x.group_start = reinterpret_cast<decltype(x.group_start)>(dlsym(h, "ncclGroupStart"));
+    x.group_end = reinterpret_cast<decltype(x.group_end)>(dlsym(h, "ncclGroupEnd"));
+    x.error_string = reinterpret_cast<decltype(x.error_string)>(dlsym(h, "ncclGetErrorString"));
+    x.ok = x.comm_init_all && x.comm_destroy && x.all_reduce && x.group_start && x.group_end && x.error_string;
+    return x;
+  }();
+  return r;
+}
+
+#define NCCLCHK(expr)                                                                     \
+  do {                                                                                    \
+    ncclResult_t r_ = (expr);                                                             \
+    if (r_ != ncclSuccess) return fail(FMCW_E_HIP, std::string(#expr) + ": " + rccl().error_string(r_)); \
+  } while (0)
+
+// contiguous shard [f0, f0 + n) of `total` items for member g of `world` (dist.py shard_range)
+void shard(int64_t total, int g, int world, int64_t& f0, int64_t& n) {
+  const int64_t base = total / world, rem = total % world;
+  f0 = g * base + std::min<int64_t>(g, rem);
+  n = base + (g < rem ? 1 : 0);
+}
+
 constexpr int kStages = 9;   // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call, 8 k_rd1p
 
 }  // namespace
@@ -93,13 +144,18 @@ struct fmcw_ctx {
   DevBuf h_iq, h_prof, h_count, h_ridx, h_rmag, h_didx, h_slow, h_cube, h_rd, h_probe;
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
   int64_t chunk_frames = 0;
-  int pipe_mode = FMCW_PIPE_AUTO, pipe_nslot = 2;
-  DevBuf fused_ctrl, fused_slots, fused_rd_slots, fused_sticky;
+  int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
   DevBuf op_gh, op_tab;                        // single-pass tables (fmcw::OP_TAB_*)
-  DevBuf op_xbuf, op_xctl;                     // single pass, pair exchange: payload and flags/XCC ids (per chunk)
   float op_gh_scale = 0.f;                     // IF_scale op_gh was built for (0 = stale)
-  bool fused_ran = false;
+  // Multi-device context (fmcw_ctx_create with n_devices > 1): this object is
+  // device 0 of the context and peers[i] a full context on device i + 1.  The
+  // host-pointer calls shard their frames (fmcw_process, fmcw_range_fft) or
+  // spectrogram segments (fmcw_stft) over all of them; the device-pointer
+  // calls act on device 0.  comms: one RCCL communicator per device
+  // (ncclCommInitAll) when the device ids are distinct.
+  std::vector<fmcw_ctx*> peers;
+  std::vector<ncclComm_t> comms;
   int timing = 0;                    // 0 off, 1 range+Doppler span + STFT launches, 2 + every K1/K2/K3
   struct Pending {
     hipEvent_t a, b;
@@ -111,6 +167,8 @@ struct fmcw_ctx {
   int64_t launches[kStages] = {};
 
   ~fmcw_ctx() {
+    for (ncclComm_t m : comms) (void)rccl().comm_destroy(m);
+    for (fmcw_ctx* q : peers) delete q;
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto& pd : pending) { (void)hipEventDestroy(pd.a); (void)hipEventDestroy(pd.b); }
@@ -261,8 +319,7 @@ int fmcw_device_count(int32_t* n) {
   return FMCW_OK;
 }
 
-int fmcw_ctx_create(int32_t device_id, fmcw_ctx** out) {
-  if (!out) return fail(FMCW_E_ARG, "out is NULL");
+static int ctx_create_one(int32_t device_id, fmcw_ctx** out) {
   *out = nullptr;
   int nd = 0;
   HIPCHK(hipGetDeviceCount(&nd));
@@ -288,6 +345,55 @@ int fmcw_ctx_create(int32_t device_id, fmcw_ctx** out) {
     return fail(FMCW_E_HIP, "stream/event creation failed");
   }
   *out = c;
+  return FMCW_OK;
+}
+
+int fmcw_ctx_create(int32_t n_devices, const int32_t* device_ids, fmcw_ctx** out) {
+  if (!out) return fail(FMCW_E_ARG, "out is NULL");
+  *out = nullptr;
+  if (n_devices < 1 || n_devices > 64) return fail(FMCW_E_ARG, "n_devices must be in [1, 64]");
+  std::vector<int> ids(n_devices);
+  for (int i = 0; i < n_devices; ++i) ids[i] = device_ids ? device_ids[i] : i;
+  fmcw_ctx* c = nullptr;
+  CHK(ctx_create_one(ids[0], &c));
+  for (int i = 1; i < n_devices; ++i) {
+    fmcw_ctx* q = nullptr;
+    const int st = ctx_create_one(ids[i], &q);
+    if (st != FMCW_OK) {
+      delete c;
+      return st;
+    }
+    c->peers.push_back(q);
+  }
+  std::vector<int> sorted = ids;
+  std::sort(sorted.begin(), sorted.end());
+  const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+  if (n_devices > 1 && distinct) {   // one communicator per device, one process
+    if (!rccl().ok) {
+      delete c;
+      return fail(FMCW_E_HIP, "RCCL (librccl.so.1) not found: needed for a context over several devices");
+    }
+    c->comms.assign(n_devices, nullptr);
+    const ncclResult_t r = rccl().comm_init_all(c->comms.data(), n_devices, ids.data());
+    if (r != ncclSuccess) {
+      c->comms.clear();
+      const std::string msg = std::string("ncclCommInitAll: ") + rccl().error_string(r);
+      delete c;
+      return fail(FMCW_E_HIP, msg);
+    }
+  }
+  *out = c;
+  return FMCW_OK;
+}
+
+int fmcw_ctx_devices(fmcw_ctx* c, int32_t* n_devices, int32_t* device_ids, int32_t* rccl_comms) {
+  if (!c || !n_devices) return fail(FMCW_E_ARG, "NULL argument");
+  *n_devices = 1 + (int32_t)c->peers.size();
+  if (device_ids) {
+    device_ids[0] = c->device;
+    for (size_t i = 0; i < c->peers.size(); ++i) device_ids[i + 1] = c->peers[i]->device;
+  }
+  if (rccl_comms) *rccl_comms = c->comms.empty() ? 0 : 1;
   return FMCW_OK;
 }
 
@@ -319,6 +425,7 @@ int fmcw_set_taps(fmcw_ctx* c, const fmcw_params* p, const float* range_win, con
   c->p = *p;
   c->taps = true;
   c->op_gh_scale = 0.f;
+  for (fmcw_ctx* q : c->peers) CHK(fmcw_set_taps(q, p, range_win, doppler_win, calib));
   return FMCW_OK;
 }
 
@@ -326,28 +433,16 @@ int fmcw_set_chunk_frames(fmcw_ctx* c, int64_t frames) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   if (frames < 0) return fail(FMCW_E_ARG, "frames < 0");
   c->chunk_frames = frames;
+  for (fmcw_ctx* q : c->peers) q->chunk_frames = frames;
   return FMCW_OK;
 }
 
-int fmcw_set_pipeline(fmcw_ctx* c, int32_t mode, int32_t nslot) {
+int fmcw_set_pipeline(fmcw_ctx* c, int32_t mode) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
-  if (mode < FMCW_PIPE_AUTO || mode > FMCW_PIPE_ONEPASS) return fail(FMCW_E_ARG, "bad pipeline mode");
-  if (nslot != 0 && (nslot < 2 || nslot > 8)) return fail(FMCW_E_ARG, "nslot must be 0 or in [2, 8]");
+  if (mode != FMCW_PIPE_AUTO && mode != FMCW_PIPE_STREAMS && mode != FMCW_PIPE_ONEPASS)
+    return fail(FMCW_E_ARG, "bad pipeline mode");
   c->pipe_mode = mode;
-  c->pipe_nslot = nslot == 0 ? 2 : nslot;
-  return FMCW_OK;
-}
-
-int fmcw_pipeline_status(fmcw_ctx* c, int32_t* status) {
-  if (!c || !status) return fail(FMCW_E_ARG, "NULL argument");
-  CHK(set_device(c));
-  *status = 0;
-  if (!c->fused_sticky.p) return FMCW_OK;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  unsigned v = 0;
-  HIPCHK(hipMemcpy(&v, c->fused_sticky.p, 4, hipMemcpyDeviceToHost));
-  if (v) HIPCHK(hipMemset(c->fused_sticky.p, 0, 4));
-  *status = (int32_t)v;
+  for (fmcw_ctx* q : c->peers) q->pipe_mode = mode;
   return FMCW_OK;
 }
 
@@ -362,7 +457,7 @@ int fmcw_timing_enable(fmcw_ctx* c, int32_t enable) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   if (enable < 0 || enable > 2) return fail(FMCW_E_ARG, "timing level must be 0, 1 or 2");
   c->timing = enable;
-  return FMCW_OK;
+  return FMCW_OK;   // device 0 only: the timers are the device-pointer calls' (benches)
 }
 
 static int timing_collect(fmcw_ctx* c) {
@@ -400,57 +495,6 @@ int fmcw_timing_reset(fmcw_ctx* c) {
 // ---------------------------------------------------------------------------
 // per-frame stages
 // ---------------------------------------------------------------------------
-// One persistent launch (kernels_fused.hip): the range cube of each frame
-// lives in a per-XCD slot instead of HBM.  d_rd == nullptr keeps the RD maps
-// in per-XCD slots too (detect is their only consumer).
-static int process_fused(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
-                         float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
-                         float* d_slow, void* d_rd, int32_t rd_dt, int64_t probe_column, float* d_probe,
-                         hipStream_t s) {
-  const int C = p->pn, NR = p->nr, ND = p->nd, ns = c->pipe_nslot;
-  const size_t words = (size_t)fmcw::fused_ctrl_words(F);
-  CHK(c->fused_ctrl.ensure(words * 4));
-  CHK(c->fused_slots.ensure((size_t)8 * ns * C * NR * 8));
-  if (!d_rd) CHK(c->fused_rd_slots.ensure((size_t)8 * ns * NR * ND * esize(rd_dt)));
-  if (!c->fused_sticky.p) {
-    CHK(c->fused_sticky.ensure(4));
-    HIPCHK(hipMemsetAsync(c->fused_sticky.p, 0, 4, s));
-  }
-  HIPCHK(hipMemsetAsync(c->fused_ctrl.p, 0, words * 4, s));
-  fmcw::FusedArgs a{};
-  a.iq = d_iq; a.in_dtype = in_dtype; a.F = F;
-  a.C = C; a.S = p->nts; a.NR = NR; a.ND = ND;
-  a.calw = c->calw.as<float4>(); a.cal_sum = c->cal_sum; a.if_scale = p->if_scale;
-  a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
-  a.rd = d_rd; a.rd_dtype = rd_dt;
-  a.rd_scale = rd_dt == FMCW_C32H ? 1.0f / ((float)NR * ND) : 1.0f;
-  a.rd_slots = d_rd ? nullptr : c->fused_rd_slots.p;
-  a.profile = d_prof;
-  a.slots = c->fused_slots.as<float2>();
-  a.nslot = ns;
-  a.ctrl = c->fused_ctrl.as<unsigned>();
-  a.spin_limit = 1u << 22;           // ~ seconds of polling: only a broken schedule gets there
-  a.sticky = c->fused_sticky.as<unsigned>();
-  {
-    const char* e = std::getenv("FMCW_FUSED_STRICT");
-    a.strict = (e && e[0] == '1') ? 1 : 0;
-  }
-  a.det.ND = ND; a.det.C = C; a.det.M = p->max_targets;
-  a.det.range_thr = p->range_thr; a.det.doppler_thr = p->doppler_thr;
-  a.det.min_d = p->min_d; a.det.max_d = p->max_d; a.det.dist_per_bin = p->dist_per_bin;
-  a.det.fallback = p->doppler_fallback_idx;
-  a.det.cube_unscale = 1.0f; a.det.rd_unscale = 1.0f / a.rd_scale;
-  a.count = d_count; a.ridx = d_ridx; a.rmag = d_rmag; a.didx = d_didx; a.slow_mag = d_slow;
-  a.probe_frame = probe_column > 0 ? (probe_column - 1) / C : -1;
-  a.probe_chirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
-  a.probe_mag = d_probe;
-  StageTimer span(c, 7, s, 1);
-  HIPCHK(fmcw::launch_fused(a, s));
-  span.done();
-  c->fused_ran = true;
-  return FMCW_OK;
-}
-
 // Per-bin linearity constants of the single-pass range stage (kernels_onepass.hip):
 // Gh[r] = DFT((cal - mean(cal)) w')[r], Hh[r] = DFT(w')[r], w' = float(IF_scale w)
 // (the values K1 uses), accumulated in float64 and rounded once.
@@ -508,8 +552,8 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
       const double a = -2.0 * M_PI * (double)((i * d) & 255) / 256.0;
       put(fmcw::OP_TAB_TWR + i * 32 + d, std::cos(a), std::sin(a));
     }
-  for (int e = 0; e < 2; ++e)                 // pair range pass: W256^(2l + e) = W1024^(4 (2l + e))
-    for (int l = 0; l < 64; ++l) put(fmcw::OP_TAB_W256 + e * 64 + l, cr[(4 * (2 * l + e)) & (NR - 1)], ci[(4 * (2 * l + e)) & (NR - 1)]);
+  for (int e = 0; e < 256; ++e)               // W256^(e d2) = W1024^(4 e d2)
+    for (int d = 0; d < 32; ++d) put(fmcw::OP_TAB_TWR2 + e * 32 + d, cr[(4 * e * d) & (NR - 1)], ci[(4 * e * d) & (NR - 1)]);
   for (int tt = 0; tt < 8; ++tt)
     for (int j = 0; j < 8; ++j)
       for (int e = 0; e < 2; ++e)
@@ -537,20 +581,12 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
                            int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
                            void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
   const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
-  // pair exchange (kernels_onepass.hip PAIR): default on; FMCW_ONEPASS_PAIR=0 selects the 8-tile range pass
-  bool pair = true;
-  if (const char* e = std::getenv("FMCW_ONEPASS_PAIR"); e && e[0] == '0') pair = false;
-  // the exchange payload is 1 MiB per frame of a chunk: chunks of at most 1024 frames
-  const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : (pair ? 1024 : 8192));
+  const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : 8192);
   constexpr int TC = fmcw::OP_TILES * fmcw::OP_CAND;
   CHK(c->op_rowpk.ensure((size_t)chunk * NR * 8));
   CHK(c->op_cidx.ensure((size_t)chunk * TC * 4));
   CHK(c->op_crows.ensure((size_t)chunk * TC * C * 4));
   CHK(c->op_fix.ensure((size_t)chunk * 4 + 16));
-  if (pair) {
-    CHK(c->op_xbuf.ensure((size_t)chunk * 8 * 8 * 16 * 64 * 16));
-    CHK(c->op_xctl.ensure((size_t)chunk * 8 * 4 * 2));
-  }
   int32_t* fix_count = c->op_fix.as<int32_t>();
   int32_t* fix_list = fix_count + 4;
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
@@ -585,14 +621,6 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;
     }
-    if (pair) {
-      a.pair = 1;
-      a.xbuf = c->op_xbuf.as<float4>();
-      a.xflag = c->op_xctl.as<unsigned>();
-      a.xcc = a.xflag + nf * 8;
-      if (const char* e = std::getenv("FMCW_ONEPASS_XMODE")) a.xmode = std::atoi(e);
-      HIPCHK(hipMemsetAsync(a.xflag, 0xFF, (size_t)nf * 8 * 4 * 2, s));   // flags and XCC ids: "not yet"
-    }
 #ifdef OP_STAMPS
     static unsigned long long* dbg = nullptr;
     const size_t nblk = (size_t)((nf + 7) / 8) * 64;
@@ -624,16 +652,6 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
                    "doppler %.2f drain %.2f (life %.2f) | avg resident %.1f\n", nblk, span / 100.0,
                    ph[0] / nblk / 100.0, ph[1] / nblk / 100.0, ph[2] / nblk / 100.0, ph[3] / nblk / 100.0,
                    ph[4] / nblk / 100.0, life / nblk / 100.0, life / span);
-      if (a.pair) {   // 6: own half done (wave 0), 7: hand-off flag seen
-        double q[3] = {0, 0, 0};
-        for (size_t i = 0; i < nblk; ++i) {
-          q[0] += (double)(h[8 * i + 6] - h[8 * i + 1]);
-          q[1] += (double)(h[8 * i + 7] - h[8 * i + 6]);
-          q[2] += (double)(h[8 * i + 2] - h[8 * i + 7]);
-        }
-        std::fprintf(stderr, "stamps pair: own half %.2f  publish+wait %.2f  receive %.2f us per block\n",
-                     q[0] / nblk / 100.0, q[1] / nblk / 100.0, q[2] / nblk / 100.0);
-      }
     }
 #endif
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
@@ -691,15 +709,6 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
     return process_onepass(c, p, d_iq, in_dtype == FMCW_C32H ? 1 : 0, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd, probe_column,
                            d_probe, s);
   }
-  const bool fusable = !d_cube && fmcw::fused_supported(NR, ND);
-  if (c->pipe_mode == FMCW_PIPE_FUSED && !fusable)
-    return fail(FMCW_E_ARG, "fused schedule: no fused kernel for this geometry, or a range cube was requested");
-  // otherwise AUTO = streams: with a 2 MiB fp32 range cube per frame two frames
-  // in flight do not fit one XCD's 4 MiB L2, so the fused schedule moves the
-  // same HBM bytes as the streams one and is slower (fused schedule)
-  if (fusable && c->pipe_mode == FMCW_PIPE_FUSED)
-    return process_fused(c, p, d_iq, in_dtype, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd,
-                         d_rd ? out_dtype : FMCW_C64, probe_column, d_probe, s);
   const int64_t chunk = c->chunk_frames > 0 ? c->chunk_frames : default_chunk(p);
   const int cube_dt = d_cube ? out_dtype : FMCW_C64;
   const int rd_dt = d_rd ? out_dtype : FMCW_C64;
@@ -963,35 +972,83 @@ int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t 
   if (L > 0x7fffffffLL) return fail(FMCW_E_ARG, "L too large for the host API");
   int64_t nseg = 0;
   int32_t nf = 0, nbo = 0;
-  CHK(fmcw_stft_sizes(L, wlen, noverlap, nfft, n_log_bins, &nseg, &nf, &nbo));
-  CHK(set_device(c));
-  hipStream_t s = c->stream;
-  const int nb = nf / 2 + 1;
-  CHK(c->s_x.ensure((size_t)L * 4));
-  CHK(c->s_list.ensure(4));
-  CHK(c->s_len.ensure(8));
-  CHK(c->s_P.ensure((size_t)nseg * nb * 4));
-  CHK(c->s_pmax.ensure(4));
-  CHK(c->s_nseg.ensure(8));
-  CHK(c->s_win.ensure((size_t)wlen * 4));
-  CHK(c->s_out.ensure((size_t)nseg * nbo * 4));
-  const int32_t zero = 0;
-  const int64_t len = L;
-  HIPCHK(hipMemcpyAsync(c->s_x.p, x, (size_t)L * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(c->s_list.p, &zero, 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(c->s_len.p, &len, 8, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(c->s_win.p, win, (size_t)wlen * 4, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(c->s_pmax.p, 0, 4, s));
-  // the whole signal is one "frame" of L samples in the compaction indirection
-  CHK(fmcw_stft_power_device(c, c->s_x.as<float>(), c->s_list.as<int32_t>(), c->s_len.as<int64_t>(), (int32_t)L,
-                             nullptr, 0, nullptr, c->s_win.as<float>(), wlen, noverlap, nf, fs, nseg, c->s_P.as<float>(),
-                             c->s_pmax.as<float>(), c->s_nseg.as<int64_t>(), s));
-  CHK(fmcw_stft_db_device(c, c->s_P.as<float>(), c->s_nseg.as<int64_t>(), nseg, nf, fs, c->s_pmax.as<float>(),
-                          n_log_bins, n_log_bins > 0 ? c->s_out.as<float>() : c->s_P.as<float>(), s));
-  const float* res = n_log_bins > 0 ? c->s_out.as<float>() : c->s_P.as<float>();
-  HIPCHK(hipMemcpyAsync(intensity, res, (size_t)nseg * nbo * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
+  CHK(fmcw_stft_sizes(L, wlen, noverlap, nfft, n_log_bins, &nseg, &nf, &nbo));   // nfft rule on the whole signal
   const int hop = wlen - noverlap;
+  const int nb = nf / 2 + 1;
+  const int world = 1 + (int)c->peers.size();
+  auto dev = [&](int g) { return g == 0 ? c : c->peers[g - 1]; };
+  // Segments are sharded contiguously over the devices; device g takes the
+  // samples its segments cover (its halo is simply the next samples of x).
+  // 1) P and the local max(P) per device
+  for (int g = 0; g < world; ++g) {
+    fmcw_ctx* d = dev(g);
+    int64_t s0, ns;
+    shard(nseg, g, world, s0, ns);
+    CHK(set_device(d));
+    hipStream_t s = d->stream;
+    const int64_t Ld = ns > 0 ? (ns - 1) * hop + wlen : 0;
+    CHK(d->s_x.ensure((size_t)std::max<int64_t>(Ld, 1) * 4));
+    CHK(d->s_list.ensure(4));
+    CHK(d->s_len.ensure(8));
+    CHK(d->s_P.ensure((size_t)std::max<int64_t>(ns, 1) * nb * 4));
+    CHK(d->s_pmax.ensure(4));
+    CHK(d->s_nseg.ensure(8));
+    CHK(d->s_win.ensure((size_t)wlen * 4));
+    CHK(d->s_out.ensure((size_t)std::max<int64_t>(ns, 1) * nbo * 4));
+    HIPCHK(hipMemsetAsync(d->s_pmax.p, 0, 4, s));
+    if (ns == 0) continue;
+    const int32_t zero = 0;
+    HIPCHK(hipMemcpyAsync(d->s_x.p, x + s0 * hop, (size_t)Ld * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d->s_list.p, &zero, 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d->s_len.p, &Ld, 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d->s_win.p, win, (size_t)wlen * 4, hipMemcpyHostToDevice, s));
+    // the shard's samples are one "frame" of Ld samples in the compaction indirection
+    CHK(fmcw_stft_power_device(d, d->s_x.as<float>(), d->s_list.as<int32_t>(), d->s_len.as<int64_t>(), (int32_t)Ld,
+                               nullptr, 0, nullptr, d->s_win.as<float>(), wlen, noverlap, nf, fs, ns, d->s_P.as<float>(),
+                               d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
+    HIPCHK(hipStreamSynchronize(s));   // the host-side scalars above go out of scope
+  }
+  // 2) the global max(P) of :282-283: RCCL all_reduce(max) across the devices
+  if (world > 1) {
+    if (!c->comms.empty()) {
+      NCCLCHK(rccl().group_start());
+      for (int g = 0; g < world; ++g) {
+        fmcw_ctx* d = dev(g);
+        CHK(set_device(d));
+        NCCLCHK(rccl().all_reduce(d->s_pmax.p, d->s_pmax.p, 1, ncclFloat32, ncclMax, c->comms[g], d->stream));
+      }
+      NCCLCHK(rccl().group_end());
+    } else {   // several contexts on ONE device (no communicator can span them): 4 bytes through the host
+      float m = 0.f;
+      for (int g = 0; g < world; ++g) {
+        float v = 0.f;
+        CHK(set_device(dev(g)));
+        HIPCHK(hipMemcpy(&v, dev(g)->s_pmax.p, 4, hipMemcpyDeviceToHost));
+        m = std::max(m, v);
+      }
+      for (int g = 0; g < world; ++g) {
+        CHK(set_device(dev(g)));
+        HIPCHK(hipMemcpy(dev(g)->s_pmax.p, &m, 4, hipMemcpyHostToDevice));
+      }
+    }
+  }
+  // 3) dB (+ log-frequency resampling) and the rows back into intensity
+  for (int g = 0; g < world; ++g) {
+    fmcw_ctx* d = dev(g);
+    int64_t s0, ns;
+    shard(nseg, g, world, s0, ns);
+    if (ns == 0) continue;
+    CHK(set_device(d));
+    hipStream_t s = d->stream;
+    CHK(fmcw_stft_db_device(d, d->s_P.as<float>(), d->s_nseg.as<int64_t>(), ns, nf, fs, d->s_pmax.as<float>(),
+                            n_log_bins, n_log_bins > 0 ? d->s_out.as<float>() : d->s_P.as<float>(), s));
+    const float* res = n_log_bins > 0 ? d->s_out.as<float>() : d->s_P.as<float>();
+    HIPCHK(hipMemcpyAsync(intensity + s0 * nbo, res, (size_t)ns * nbo * 4, hipMemcpyDeviceToHost, s));
+  }
+  for (int g = 0; g < world; ++g) {
+    CHK(set_device(dev(g)));
+    HIPCHK(hipStreamSynchronize(dev(g)->stream));
+  }
   for (int64_t i = 0; i < nseg; ++i) T[i] = (float)(((double)i * hop + wlen / 2.0) / fs);   // spectrogram T
   if (n_log_bins > 0) {
     std::vector<int32_t> idx;
@@ -1008,9 +1065,9 @@ int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t 
 // ---------------------------------------------------------------------------
 // host-pointer per-frame API
 // ---------------------------------------------------------------------------
-int fmcw_process(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F, float* prof,
-                 int32_t* count, int32_t* ridx, float* rmag, int32_t* didx, float* slow, float* cube, float* rd,
-                 int64_t probe_column, float* probe) {
+static int process_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F,
+                            float* prof, int32_t* count, int32_t* ridx, float* rmag, int32_t* didx, float* slow,
+                            float* cube, float* rd, int64_t probe_column, float* probe) {
   CHK(check_ctx(c, p));
   if (F < 0) return fail(FMCW_E_ARG, "F < 0");
   if (F == 0) return FMCW_OK;
@@ -1043,16 +1100,11 @@ int fmcw_process(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_d
   if (rd) HIPCHK(hipMemcpyAsync(rd, c->h_rd.p, (size_t)F * NR * ND * 8, hipMemcpyDeviceToHost, s));
   if (probe) HIPCHK(hipMemcpyAsync(probe, c->h_probe.p, (size_t)NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  if (c->fused_ran) {
-    int32_t st = 0;
-    CHK(fmcw_pipeline_status(c, &st));
-    if (st) return fail(FMCW_E_HIP, "fused schedule: a bounded wait timed out; results are invalid");
-  }
   return FMCW_OK;
 }
 
-int fmcw_range_fft(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F, float* cube,
-                   float* prof) {
+static int range_fft_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F,
+                              float* cube, float* prof) {
   CHK(check_ctx(c, p));
   if (F < 0) return fail(FMCW_E_ARG, "F < 0");
   if (F == 0) return FMCW_OK;
@@ -1069,6 +1121,69 @@ int fmcw_range_fft(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in
   HIPCHK(hipMemcpyAsync(prof, c->h_prof.p, (size_t)F * NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   return FMCW_OK;
+}
+
+}  // extern "C"
+
+// Run fn(device context, shard index, f0, n) on every device of the context,
+// one host thread per device (their H2D copies, kernels and D2H copies then
+// overlap), over contiguous shards of `total` items.  The first failing
+// device's status and message are returned.
+template <typename Fn>
+static int over_devices(fmcw_ctx* c, int64_t total, Fn&& fn) {
+  const int world = 1 + (int)c->peers.size();
+  if (world == 1) return fn(c, 0, (int64_t)0, total);
+  std::vector<int> st(world, FMCW_OK);
+  std::vector<std::string> msg(world);
+  std::vector<std::thread> th;
+  for (int g = 0; g < world; ++g) {
+    th.emplace_back([&, g] {
+      int64_t f0, n;
+      shard(total, g, world, f0, n);
+      fmcw_ctx* d = g == 0 ? c : c->peers[g - 1];
+      st[g] = n > 0 ? fn(d, g, f0, n) : FMCW_OK;
+      if (st[g] != FMCW_OK) msg[g] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (int g = 0; g < world; ++g)
+    if (st[g] != FMCW_OK) return fail(st[g], "device " + std::to_string(g) + ": " + msg[g]);
+  return FMCW_OK;
+}
+
+extern "C" {
+
+int fmcw_process(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F, float* prof,
+                 int32_t* count, int32_t* ridx, float* rmag, int32_t* didx, float* slow, float* cube, float* rd,
+                 int64_t probe_column, float* probe) {
+  CHK(check_ctx(c, p));
+  if (F < 0) return fail(FMCW_E_ARG, "F < 0");
+  if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
+  if (probe_column < 0 || probe_column > F * (int64_t)p->pn) return fail(FMCW_E_ARG, "probe_column out of range");
+  const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
+  const size_t fin = (size_t)C * S * esize(in_dtype);
+  // frames are independent: each device takes a contiguous shard and writes its
+  // rows of every output in place (the range_speed concatenation of :386-389 is
+  // the frame order itself); the probed column lives on one shard
+  return over_devices(c, F, [&](fmcw_ctx* d, int, int64_t f0, int64_t n) {
+    const int64_t pc = probe_column > f0 * C && probe_column <= (f0 + n) * C ? probe_column - f0 * C : 0;
+    return process_host_one(d, p, static_cast<const char*>(iq) + f0 * fin, in_dtype, n, prof + f0 * NR, count + f0,
+                            ridx + f0 * M, rmag + f0 * M, didx + f0 * M, slow + f0 * C,
+                            cube ? cube + f0 * (size_t)C * NR * 2 : nullptr, rd ? rd + f0 * (size_t)NR * ND * 2 : nullptr,
+                            pc, pc ? probe : nullptr);
+  });
+}
+
+int fmcw_range_fft(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F, float* cube,
+                   float* prof) {
+  CHK(check_ctx(c, p));
+  if (F < 0) return fail(FMCW_E_ARG, "F < 0");
+  if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
+  const size_t fin = (size_t)p->pn * p->nts * esize(in_dtype);
+  return over_devices(c, F, [&](fmcw_ctx* d, int, int64_t f0, int64_t n) {
+    return range_fft_host_one(d, p, static_cast<const char*>(iq) + f0 * fin, in_dtype, n,
+                              cube + f0 * (size_t)p->pn * p->nr * 2, prof + f0 * p->nr);
+  });
 }
 
 int fmcw_synth_device(fmcw_ctx* c, const fmcw_params* p, int64_t frame0, int64_t F, void* d_iq, int32_t dtype,

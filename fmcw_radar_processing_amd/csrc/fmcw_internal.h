@@ -54,49 +54,13 @@ struct DetectArgs {
   float* probe_mag;        // [NR]
 };
 
-// detection constants shared by k_detect and the fused kernel (frame_ops.h)
+// detection constants shared by k_detect and k_detect_1p (frame_ops.h)
 struct DetectParams {
   int ND, C, M;
   float range_thr, doppler_thr, min_d, max_d, dist_per_bin;
   int fallback;
   float cube_unscale, rd_unscale;
 };
-
-// persistent XCD-local range+Doppler+detect (kernels_fused.hip)
-struct FusedArgs {
-  const void* iq;          // [F][C][S]
-  int in_dtype;
-  int64_t F;
-  int C, S, NR, ND;
-  const float4* calw;
-  float2 cal_sum;
-  float if_scale;
-  const float2* tw_nr;     // [NR]
-  const float2* tw_nd;     // [ND]
-  const float* wd;         // [C]
-  void* rd;                // [F][NR][ND], or nullptr: RD lives in per-XCD slots (rd_slots)
-  int rd_dtype;
-  float rd_scale;
-  void* rd_slots;          // [8][nslot][NR][ND] of rd_dtype when rd == nullptr
-  float* profile;          // [F][NR]
-  float2* slots;           // [8 XCDs][nslot][C][NR] fp32 cube slots
-  int nslot;               // >= 2
-  unsigned* ctrl;          // zeroed per launch: 8 heads (128 B apart), k1done[F], k2done[F], done[F], err
-  unsigned spin_limit;
-  unsigned* sticky;        // set to 1 on a spin timeout; cleared only by fmcw_pipeline_status
-  int strict;              // 1: agent release/acquire at every hand-off (placement-independent form)
-  DetectParams det;
-  int32_t* count;
-  int32_t* ridx;
-  float* rmag;
-  int32_t* didx;
-  float* slow_mag;
-  int64_t probe_frame;     // global frame, -1 = none
-  int probe_chirp;
-  float* probe_mag;
-};
-
-inline int64_t fused_ctrl_words(int64_t F) { return 256 + 3 * F + 1; }
 
 // Single-pass range+Doppler (kernels_onepass.hip).  Frame f is split into
 // OP_TILES range tiles: tile t owns the bins r == t (mod OP_TILES) for every
@@ -107,8 +71,8 @@ constexpr int OP_CAND = 2;           // slow-time candidate rows kept per tile
 constexpr int OP_TAB_LANE = 0;       // [6][64]: DIF twiddles of spans 32..2 (1 on clear lanes of spans 8..2), W128^lane_bin(l)
 constexpr int OP_TAB_TWR = 384;      // [8][32]: W256^(i d2)
 constexpr int OP_TAB_CST = 640;      // [8 t][8 j][2 e][64 l]: w'[n] W1024^(t n), n = 2l + e + 128j
-constexpr int OP_TAB_W256 = 640 + 8 * 1024;   // [2 e][64 l]: W256^(2l + e) (pair range pass)
-constexpr int OP_TAB_SIZE = OP_TAB_W256 + 128;
+constexpr int OP_TAB_TWR2 = 640 + 8 * 1024;    // [256 e][32 d2]: W256^(e d2) (rotated chirp order)
+constexpr int OP_TAB_SIZE = OP_TAB_TWR2 + 256 * 32;
 
 struct OnePassArgs {
   const void* iq;          // [F][C][S] c64, or c32h when h
@@ -132,12 +96,6 @@ struct OnePassArgs {
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
   unsigned long long* dbg; // diagnostic builds only (-DOP_STAMPS): [blocks][8] s_memrealtime stamps
-  int pair;                // pair-exchange range pass (kernels_onepass.hip, PAIR)
-  float4* xbuf;            // pair: [F][8 t][8 w][16 i][64 l] {slot0, slot1} of tile t ^ 4, from tile t's chirps
-  unsigned* xflag;         // pair: [F][8] hand-off flags (1 = same-XCD publish, 2 = released), 0xFFFFFFFF before
-  unsigned* xcc;           // pair: [F][8] XCC_ID of each tile's workgroup, 0xFFFFFFFF before
-  int xmode;               // pair test knob (FMCW_ONEPASS_XMODE): 0 normal, 1 always release the
-                           // hand-off, 2 never take the partner's half (recompute it locally)
 };
 
 struct Detect1pArgs {
@@ -235,8 +193,6 @@ hipError_t launch_stft_db(const StftDbArgs& a, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s);
 
-hipError_t launch_fused(const FusedArgs& a, hipStream_t s);
-bool fused_supported(int nr, int nd);
 
 bool range_size_supported(int nr);
 bool doppler_size_supported(int nd);

@@ -1,6 +1,6 @@
-// frame_ops.h -- per-frame stage bodies shared by the stand-alone kernels
-// (kernels_frame.hip: K1/K2/K3 launched as a 3-stream chunk pipeline) and the
-// persistent XCD-local fused kernel (kernels_fused.hip).
+// frame_ops.h -- per-frame stage bodies of the streams schedule
+// (kernels_frame.hip: K1/K2/K3 launched as a 3-stream chunk pipeline); the
+// peak rule is shared with the single pass (kernels_onepass.hip).
 //
 //   range_team     radar_processing.m:203-205 (+:207 store): one chirp per team
 //   doppler_tile   :210/:265 profile, :216-219 Doppler (mean over all PN,
@@ -8,10 +8,9 @@
 //   detect_frame   :211 f_search_peak rule, :227-239 Doppler
 //                  index, :257-259 slow-time row, :410-411 probe column
 //
-// Load policy NT: the fused kernel reads data another workgroup of the SAME
-// XCD just wrote with `nt` loads, which bypass the CU's vector L1 and are
-// served by the XCD's L2 (MI355X_MICROARCH.md, visibility table), so no L1
-// invalidate is needed for that hand-off.
+// Load policy NT (template flag): `nt` loads bypass the CU's vector L1 and are
+// served by the XCD's L2 (MI355X_MICROARCH.md, visibility table).  The
+// stand-alone kernels read data written by an earlier launch and use plain loads.
 #pragma once
 #include <climits>
 

@@ -143,8 +143,7 @@ __global__ __launch_bounds__(256) void k_detect(DetectArgs a) {
 // dispatch
 // ---------------------------------------------------------------------------
 // 16-byte lane-pair access in K2 (FMCW_PAIR=1).  Off by default: on MI355X the
-// 8-byte cyclic path measured slightly faster, and it shares the
-// fused kernel's summation order, so both schedules agree bit for bit.
+// 8-byte cyclic path measured slightly faster.
 static bool pair_access_enabled() {
   const char* e = getenv("FMCW_PAIR");
   return e && e[0] == '1';

@@ -317,15 +317,10 @@ __device__ __forceinline__ void dft32p(c2 (&v)[32]) {
 // LDS image of k_rd1p.
 struct Lds1p {
   c2 t1[256 * 64];         // slot-1 tile [chirp][lane]; then the corner turn
-  f4v gh[4][64];           // {Gh, Hh} of lane l's bins (lane order: conflict-free reads):
-                           //   single tile: [0] r0(l), [1] r1(l) of tile t
-                           //   pair:        [0], [1] of tile p, [2], [3] of tile p + 4
+  f4v gh[2][64];           // {Gh, Hh} of lane l's bins r0(l), r1(l) (lane order: conflict-free reads)
   float red[2][NW][3][64]; // per-wave {sum.re, sum.im, max |X|^2} of each row over the wave's chirps
   float cand[OP_CAND][256];// candidate rows |X|^2 as [wave][k2] (chirp w + 8 k2), written out coalesced
-  int xok;                 // pair: the partner's half arrived (else it is recomputed here)
 };
-
-constexpr int XTMO = 20000;    // pair: bounded wait for the partner, s_memrealtime ticks (100 MHz): 200 us
 
 }  // namespace op
 
@@ -333,31 +328,11 @@ constexpr int XTMO = 20000;    // pair: bounded wait for the partner, s_memrealt
 // k_rd1p: one workgroup (8 waves, 2 per SIMD, 256 VGPRs per lane) = one range
 // tile of one frame.  FULL: S == NR (no zero padding, no masking).
 //
-// PAIR (the default for complex64 / fp16 at NR 1024, PN 256): the range pass
-// of tile t = p + 4h (p < 4, h < 2) covers only chirp half h, but computes the
-// 256 bins r == p (mod 4) of each of its chirps -- its own tile's 128 bins
-// (r == t mod 8) and those of its partner tile t ^ 4.  The partner's bins go
-// to the partner workgroup through the XCD's L2 (128 KiB each way), so every
-// sample is read by 4 workgroups instead of 8 and stage A runs once per
-// (sample, p) instead of once per (sample, t):
-//   n = a + 256 b (a < 256, b < 4), r = p + 4 m:
-//   X[p + 4m] = sum_a W256^(a m) A[a],   A[a] = sum_b y[a + 256 b] W1024^(p (a + 256 b))
-//   a = a' + 128 q:  even m = 2m': 128-point FFT of A[a'] + A[a' + 128]            -> tile p
-//                    odd  m:      128-point FFT of (A[a'] - A[a' + 128]) W256^a'    -> tile p + 4
-// Hand-off (placement-independent, MI355X_MICROARCH.md visibility rules): plain
-// 16-byte stores, every wave drains (vmcnt 0), barrier, then one lane raises
-// the workgroup's flag with an agent-scope store -- after an agent release
-// fence unless the partner has announced the same XCC_ID (then the bytes are
-// already in the one L2 both read).  The consumer polls the partner's flag
-// (relaxed agent load, bounded) and reads the bytes with sc1 loads (past its
-// L1).  A partner that does not arrive within XTMO is not waited for: its half
-// is recomputed locally (same arithmetic), so no schedule can deadlock.
 // ---------------------------------------------------------------------------
-template <bool FULL, bool H, bool PAIR>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
+template <bool FULL, bool H>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
 __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   using namespace op;
   constexpr int CPW = 32, C = NW * CPW, ND = C;  // wave w owns chirps w + 8 k2, k2 < 32
-  constexpr int HPW = CPW / 2;                   // pair: chirps per wave in one half
   __shared__ __attribute__((aligned(16))) Lds1p L;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -370,29 +345,28 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
 #ifdef OP_STAMPS
   if (tid == 0) a.dbg[(int64_t)b * 8] = __builtin_amdgcn_s_memrealtime();
 #endif
-  const int p4 = t & 3, h = t >> 2, tq = t ^ 4;  // pair: bins r == p4 (mod 4), chirp half h, partner tile
-  unsigned xcc = 0;
-  if constexpr (PAIR) {
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    if (tid == 0) __hip_atomic_store(a.xcc + f * 8 + t, xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+#ifndef OP_ROT
+#define OP_ROT 1
+#endif
+  // Tile t walks its chirp groups rotated by rs = OP_ROT * t groups (register k2
+  // holds chirp w + 8 ((k2 + rs) mod 32)): at any moment the 8 tiles of a frame
+  // first-touch 8 different groups instead of all waiting on the same HBM miss,
+  // and each group is re-read from L2 within 8 steps (measured: 4 % faster than
+  // no rotation; 4 groups per tile overflows the L2 and is 35 % slower).
+  const int rs = (OP_ROT * t) & 31;
 
   // Per-tile tables come from host-built arrays laid out in lane order
   // (fmcw_api.cpp build_onepass_gh), so every table read is a coalesced
   // 512-byte wave access: gathers here would cost the L2 as many requests as
   // the frame itself.
   const c2* __restrict__ tab = reinterpret_cast<const c2*>(a.tab);
-  {
-    const int tg = PAIR ? p4 + 4 * (tid >> 7) : t;           // pair: tiles p4 and p4 + 4
-    if (tid < (PAIR ? 256 : 128)) L.gh[tid >> 6][lane] = reinterpret_cast<const f4v*>(a.gh)[(2 * tg + ((tid >> 6) & 1)) * 64 + lane];
-  }
-  // stage-A constants c_ts[n] = w'[n] W1024^(ts n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
-  const int ts = PAIR ? p4 : t;
+  if (tid < 128) L.gh[tid >> 6][lane] = reinterpret_cast<const f4v*>(a.gh)[(2 * t + (tid >> 6)) * 64 + lane];
+  // stage-A constants c_t[n] = w'[n] W1024^(t n), n = 2 lane + e + 128 j (0 beyond S: fft(., Nr) zero-padding)
   c2 cst[16];
 #pragma unroll
   for (int j = 0; j < 8; ++j)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) cst[2 * j + e] = tab[OP_TAB_CST + ((ts * 8 + j) * 2 + e) * 64 + lane];
+    for (int e = 0; e < 2; ++e) cst[2 * j + e] = tab[OP_TAB_CST + ((t * 8 + j) * 2 + e) * 64 + lane];
   c2 twh[5];                                     // spans 32, 16 (every lane), 8, 4, 2 (1 on clear lanes)
   float sg[6];                                   // spans 32 .. 1
 #pragma unroll
@@ -454,22 +428,23 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     X1 = cmac_a(R0 - ow - g1.xy, nmx, g1.zw);    // bin r1 (slot 1)
   };
 #ifndef OP_RING
-#define OP_RING 2
+#define OP_RING 3
 #endif
   constexpr int RING = OP_RING;                  // chirps in registers: RING - 1 in flight while one is consumed
+                                                 // (3: 1 % over 2 with the rotation; 4 spills)
   c2 tile0[CPW];                                 // slot 1 goes to LDS (L.t1)
 
-  if constexpr (!PAIR) {
+  {
     c2 cs7[2];                                   // rotated copies for the last, compiler-visible MAC
     cs7[0] = c2{-cst[14].y, cst[14].x};
     cs7[1] = c2{-cst[15].y, cst[15].x};
     TP buf[RING][8];
 #pragma unroll
-    for (int i = 0; i < RING - 1; ++i) ld_chirp(w + NW * i, buf[i]);
+    for (int i = 0; i < RING - 1; ++i) ld_chirp(w + NW * ((i + rs) & (CPW - 1)), buf[i]);
 #pragma unroll
     for (int k2 = 0; k2 < CPW; ++k2) {
-      const int k = w + NW * k2;
-      if (k2 + RING - 1 < CPW) ld_chirp(k + NW * (RING - 1), buf[(k2 + RING - 1) % RING]);
+      const int k = w + NW * k2;                 // register order (chirp w + 8 ((k2 + rs) mod 32))
+      if (k2 + RING - 1 < CPW) ld_chirp(w + NW * ((k2 + RING - 1 + rs) & (CPW - 1)), buf[(k2 + RING - 1) % RING]);
       f4v x[8];
       widen(buf[k2 % RING], x);
       // stage A: sum_b x[a + 128 b] c_t[a + 128 b], straight from the loads
@@ -491,98 +466,6 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       tile0[k2] = X0;
       L.t1[k * 64 + lane] = X1;
     }
-  } else {
-    const c2 w256a = tab[OP_TAB_W256 + lane], w256b = tab[OP_TAB_W256 + 64 + lane];   // W256^(2 lane + e)
-    // range pass over chirp half hh: own tile's bins -> own[] (slot 0) and L.t1 (slot 1);
-    // the partner tile's bins -> the exchange buffer when xs
-    f4v* __restrict__ xout = reinterpret_cast<f4v*>(a.xbuf) + ((f * 8 + t) * NW + w) * (int64_t)(HPW * 64) + lane;
-    auto range_half = [&](int hh, c2 (&own)[HPW], bool xs) {
-      const int kb = w + NW * HPW * hh;           // chirp of step i: kb + NW i
-      TP buf[RING][8];
-#pragma unroll
-      for (int i = 0; i < RING - 1; ++i) ld_chirp(kb + NW * i, buf[i]);
-#pragma unroll
-      for (int i = 0; i < HPW; ++i) {
-        const int k = kb + NW * i;
-        if (i + RING - 1 < HPW) ld_chirp(k + NW * (RING - 1), buf[(i + RING - 1) % RING]);
-        f4v x[8];
-        widen(buf[i % RING], x);
-        // stage A: A[a' + 128 q] = sum_b x[a' + 128 q + 256 b] c_p[.], q = j & 1, b = j >> 1
-        c2 A00 = cmul_a(x[0].xy, cst[0]), A10 = cmul_a(x[0].zw, cst[1]);
-        c2 A01 = cmul_a(x[1].xy, cst[2]), A11 = cmul_a(x[1].zw, cst[3]);
-        f4v s4 = x[0] + x[1];
-#pragma unroll
-        for (int j = 2; j < 8; j += 2) {
-          A00 = cmac_a(A00, x[j].xy, cst[2 * j]);
-          A10 = cmac_a(A10, x[j].zw, cst[2 * j + 1]);
-          A01 = cmac_a(A01, x[j + 1].xy, cst[2 * j + 2]);
-          A11 = cmac_a(A11, x[j + 1].zw, cst[2 * j + 3]);
-          s4 += x[j] + x[j + 1];
-        }
-        // radix 2 over q (compiler-visible producers for the DPP stages)
-        c2 E0 = A00 + A01, E1 = A10 + A11;                   // even m: tile p
-        c2 O0 = cmv(A00 - A01, w256a), O1 = cmv(A10 - A11, w256b);   // odd m: tile p + 4
-        fft128(E0, E1);
-        fft128(O0, O1);
-        const c2 nmx = wave_sum_c(s4.xy + s4.zw) * ninvS;
-        c2 XE0, XE1, XO0, XO1;
-        finish(E0, E1, nmx, L.gh[0][lane], L.gh[1][lane], XE0, XE1);
-        finish(O0, O1, nmx, L.gh[2][lane], L.gh[3][lane], XO0, XO1);
-        own[i] = h ? XO0 : XE0;
-        L.t1[k * 64 + lane] = h ? XO1 : XE1;
-        if (xs) {
-          const c2 y0 = h ? XE0 : XO0, y1 = h ? XE1 : XO1;
-          xout[i * 64] = f4v{y0.x, y0.y, y1.x, y1.y};
-        }
-      }
-    };
-    c2 own[HPW], rcv[HPW];
-    range_half(h, own, true);
-    stamp(6);
-    // hand-off: publish this half of the partner's tile, then take the partner's half of ours
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave drains its stores
-    __syncthreads();
-    if (tid == 0) {
-      unsigned v = 1;
-      if (a.xmode == 1 || __hip_atomic_load(a.xcc + f * 8 + tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != xcc) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // partner elsewhere (or not started): write back L2
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        v = 2;
-      }
-      __hip_atomic_store(a.xflag + f * 8 + t, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      int ok = 0;
-      for (; a.xmode != 2;) {                      // xmode 2 (test knob): never take the partner's half
-        const unsigned q = __hip_atomic_load(a.xflag + f * 8 + tq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (q == 1u || q == 2u) { ok = 1; break; }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > (uint64_t)XTMO) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      L.xok = ok;
-    }
-    __syncthreads();
-    stamp(7);
-    const int kq = w + NW * HPW * (1 - h);         // partner half: chirps kq + NW i
-    if (__builtin_amdgcn_readfirstlane(L.xok)) {
-      const f4v* src = reinterpret_cast<const f4v*>(a.xbuf) + ((f * 8 + tq) * NW + w) * (int64_t)(HPW * 64) + lane;
-      f4v v[HPW];
-#pragma unroll
-      for (int i = 0; i < HPW; ++i)                 // sc1: past this CU's L1 (never a stale copy)
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[i]) : "v"(src + i * 64) : "memory");
-      asm volatile("s_waitcnt vmcnt(0)"
-                   : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
-                     "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
-                   :: "memory");
-#pragma unroll
-      for (int i = 0; i < HPW; ++i) {
-        rcv[i] = c2{v[i].x, v[i].y};
-        L.t1[(kq + NW * i) * 64 + lane] = c2{v[i].z, v[i].w};
-      }
-    } else {
-      range_half(1 - h, rcv, false);              // partner absent: the same arithmetic here
-    }
-#pragma unroll
-    for (int k2 = 0; k2 < CPW; ++k2) tile0[k2] = ((k2 < HPW) == (h == 0)) ? own[k2 % HPW] : rcv[k2 % HPW];
   }
 
   // ---------------- per-row reductions over the 8 waves --------------------
@@ -669,7 +552,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   // 8-point DFT over the waves (W8^(w d1)).
   auto pre = [&](c2 (&x)[CPW], c2 mu) {
 #pragma unroll
-    for (int k2 = 0; k2 < CPW; ++k2) x[k2] = (x[k2] - mu) * sload(a.wd, w + NW * k2);   // :218 (X - mean) .* 2chebwin
+    for (int k2 = 0; k2 < CPW; ++k2) x[k2] = (x[k2] - mu) * sload(a.wd, w + NW * ((k2 + rs) & (CPW - 1)));   // :218 (X - mean) .* 2chebwin
     dft32p(x);
   };
   c2* stg = L.t1;                                // [wave][row lane][d2 ^ (lane & 31)]: conflict-free both ways
@@ -677,6 +560,14 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   c2 twr[NW];                                    // W256^(i d2o): the inter-stage twiddle, applied by the reader
 #pragma unroll
   for (int i = 1; i < NW; ++i) twr[i] = tab[OP_TAB_TWR + i * 32 + d2o];
+  // rotated registers (register r holds chirp group g = r + rs mod 32):
+  //   sum_g x_g W32^(g d2) = W32^(rs d2) sum_r x_(r + rs) W32^(r d2),
+  // so each wave's DFT32 is multiplied by W32^(rs d2) = W256^(8 rs d2), folded into the
+  // reader's twiddle (wave 0 included)
+  if (rs) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) twr[i] = tab[OP_TAB_TWR2 + ((i + 8 * rs) & 255) * 32 + d2o];
+  }
   // max / min over the 32 lanes of a row (DPP: xor 1, xor 2, then mirrors on
   // group-uniform values, then the 16-lane row swap)
   auto row_max = [&](int v) {
@@ -708,6 +599,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
       for (int i = 0; i < NW; ++i) v[i] = stg[(i * 64 + lb) * CPW + (d2o ^ (lb & 31))];
 #pragma unroll
       for (int i = 1; i < NW; ++i) v[i] = cmul_a(v[i], twr[i]);
+      if (rs) v[0] = cmul_a(v[0], twr[0]);
       dft8p(v);
       const int r = t + 8 * lane_bin(lb) + 512 * sl;
       // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element e = d2o + 32 d1s
@@ -751,7 +643,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
 #pragma unroll
   for (int c = 0; c < OP_CAND; ++c)
     if (csel[c] >= 0 && tid < C)
-      a.cand_rows[((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C + tid] = L.cand[c][(tid % NW) * CPW + tid / NW];
+      a.cand_rows[((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C + tid] = L.cand[c][(tid % NW) * CPW + ((tid / NW - rs) & (CPW - 1))];
   post(0);                                       // its LDS reads and stores overlap slot 1's DFT arithmetic
   pre(tile1, mu1);
   __syncthreads();                               // B4: slot-0 corner turn read out
@@ -911,19 +803,15 @@ bool onepass_supported(int nts, int pn, int nr, int nd) {
 hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s) {
   if (a.F <= 0) return hipSuccess;
   if (!onepass_supported(a.S, a.C, op::NR, a.C)) return hipErrorInvalidValue;
-  if (a.pair && (!a.xbuf || !a.xflag || !a.xcc)) return hipErrorInvalidValue;
   const unsigned blocks = (unsigned)(((a.F + 7) / 8) * 64);
   const dim3 g(blocks), bl(64 * op::NW);
-#define FMCW_OP_LAUNCH(FU, HH, PP) hipLaunchKernelGGL((k_rd1p<FU, HH, PP>), g, bl, 0, s, a)
-  const bool full = a.S == op::NR;
-  if (a.pair) {
-    if (full) { if (a.h) FMCW_OP_LAUNCH(true, true, true); else FMCW_OP_LAUNCH(true, false, true); }
-    else { if (a.h) FMCW_OP_LAUNCH(false, true, true); else FMCW_OP_LAUNCH(false, false, true); }
+  if (a.S == op::NR) {
+    if (a.h) hipLaunchKernelGGL((k_rd1p<true, true>), g, bl, 0, s, a);
+    else hipLaunchKernelGGL((k_rd1p<true, false>), g, bl, 0, s, a);
   } else {
-    if (full) { if (a.h) FMCW_OP_LAUNCH(true, true, false); else FMCW_OP_LAUNCH(true, false, false); }
-    else { if (a.h) FMCW_OP_LAUNCH(false, true, false); else FMCW_OP_LAUNCH(false, false, false); }
+    if (a.h) hipLaunchKernelGGL((k_rd1p<false, true>), g, bl, 0, s, a);
+    else hipLaunchKernelGGL((k_rd1p<false, false>), g, bl, 0, s, a);
   }
-#undef FMCW_OP_LAUNCH
   return hipGetLastError();
 }
 

@@ -39,16 +39,29 @@ def _host_iq(iq: np.ndarray):
 
 
 class Engine:
-    """fmcw_ctx on HIP device ``device`` (no CPU fallback: raises if absent)."""
+    """fmcw_ctx on HIP device ``device`` -- an int, or a list of device ids for
+    one context over several GPUs (the host-array calls then shard their work
+    over them; include/fmcw.h fmcw_ctx_create).  No CPU fallback: raises if a
+    device is absent."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int | list | tuple = 0):
         self.lib = _lib.load()
+        ids = [int(device)] if isinstance(device, int) else [int(d) for d in device]
+        arr = (ct.c_int32 * len(ids))(*ids)
         h = ct.c_void_p()
-        check(self.lib.fmcw_ctx_create(int(device), ct.byref(h)))
+        check(self.lib.fmcw_ctx_create(len(ids), arr, ct.byref(h)))
         self.h = h
-        self.device = device
+        self.device = ids[0]
+        self.devices = ids
         self.cfg: FmcwConfig | None = None
         self.p = None
+
+    def device_info(self) -> dict:
+        """{'devices': [...], 'rccl': bool} of this context."""
+        n, rc = ct.c_int32(), ct.c_int32()
+        ids = (ct.c_int32 * 64)()
+        check(self.lib.fmcw_ctx_devices(self.h, ct.byref(n), ids, ct.byref(rc)))
+        return {"devices": list(ids[: n.value]), "rccl": bool(rc.value)}
 
     def close(self):
         if getattr(self, "h", None):
@@ -76,15 +89,9 @@ class Engine:
     def set_chunk_frames(self, n: int) -> None:
         check(self.lib.fmcw_set_chunk_frames(self.h, int(n)))
 
-    def set_pipeline(self, mode: int, nslot: int = 0) -> None:
-        """FMCW_PIPE_AUTO / _STREAMS / _FUSED / _ONEPASS (include/fmcw.h); nslot cube slots per XCD."""
-        check(self.lib.fmcw_set_pipeline(self.h, int(mode), int(nslot)))
-
-    def pipeline_status(self) -> int:
-        """0, or 1 when a fused launch since the last query hit a bounded-wait timeout."""
-        st = ct.c_int32(0)
-        check(self.lib.fmcw_pipeline_status(self.h, ct.byref(st)))
-        return st.value
+    def set_pipeline(self, mode: int) -> None:
+        """FMCW_PIPE_AUTO / _STREAMS / _ONEPASS (include/fmcw.h)."""
+        check(self.lib.fmcw_set_pipeline(self.h, int(mode)))
 
     # ---- host-array API --------------------------------------------------------
     def process(self, iq: np.ndarray, want_cube: bool = False, want_rd: bool = False,

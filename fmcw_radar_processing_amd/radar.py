@@ -90,29 +90,38 @@ def write_json(path: str, obj: dict) -> str:
 def write_outputs_no(out_dir: str, filename: str, cfg: P.FmcwConfig, per: dict, spec: dict,
                      meas: dict, frame_count: int, probe_frame_index: int, probe_mag,
                      upload: Callable[[str], None] | None = None) -> list:
-    """:302-436: the four JSON files of the 'no' branch."""
+    """:302-436: the four JSON files of the 'no' branch, each uploaded right after
+    it is written.  ``probe_mag`` None: the cube has fewer than ``probe_frame_index``
+    columns, and -- as the reference at :411 -- the fourth file fails after the
+    first three were written and uploaded."""
     paths = []
+
+    def emit(path, obj):                                        # write, then upload (:315-328 and friends)
+        write_json(path, obj)
+        if upload:
+            upload(path)
+        return path
+
     # :306-328 spectrogram_data.json
-    paths.append(write_json(os.path.join(out_dir, "spectrogram_data.json"), {
+    paths.append(emit(os.path.join(out_dir, "spectrogram_data.json"), {
         "time": spec["time"], "frequency": spec["frequency"],
         "intensity": spec["intensity"],                          # 1024 x nseg (bins down the rows)
         "title": "All Frames - Log-Scaled Spectrogram", "xLabel": "Time (s)", "yLabel": "Frequency (Hz)"}))
     # :355-377 <filename>_range_fft_data.json
     time_axis = np.arange(frame_count) * 0.15
-    paths.append(write_json(os.path.join(out_dir, f"{filename}_range_fft_data.json"), {
+    paths.append(emit(os.path.join(out_dir, f"{filename}_range_fft_data.json"), {
         "time_axis": time_axis, "array_bin_range": cfg.array_bin_range,
         "range_tx1rx1_max_abs": matlab_squeeze_2d(per["profile"].T),   # Nr x F
         "filename": filename}))
     # :379-407 <filename>_range_speed_data.json
-    paths.append(write_json(os.path.join(out_dir, f"{filename}_range_speed_data.json"), {
+    paths.append(emit(os.path.join(out_dir, f"{filename}_range_speed_data.json"), {
         "time_axis": time_axis, "range": meas["range"], "speed": meas["speed"], "filename": filename}))
     # :409-436 <filename>_fft_data.json (linear column 100 of the Nr x PN x F cube)
-    paths.append(write_json(os.path.join(out_dir, f"{filename}_fft_data.json"), {
+    if probe_mag is None:                                       # :411 range_tx1rx1_complete(:,100)
+        raise IndexError(f"Index in position 2 exceeds array bounds (must not exceed {cfg.pn * frame_count}).")
+    paths.append(emit(os.path.join(out_dir, f"{filename}_fft_data.json"), {
         "range_bins": np.arange(cfg.nr), "magnitude": np.asarray(probe_mag, np.float64),
         "frame_index": probe_frame_index, "filename": filename}))
-    if upload:
-        for p_ in paths:
-            upload(p_)
     return paths
 
 
@@ -155,16 +164,16 @@ def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_
 
 def _run_no(eng, cfg, frames, F, filename, out_dir, upload):
     probe_col = 100                                                     # :410 fr_idx = 100
-    if probe_col > F * cfg.pn:
-        raise IndexError("Index exceeds the number of array elements (range_tx1rx1_complete(:,100))")
-    per = eng.process(frames, probe_column=probe_col)                   # :197-261, :265
+    have_probe = probe_col <= F * cfg.pn                                # else :411 fails after three files
+    per = eng.process(frames, probe_column=probe_col if have_probe else 0)   # :197-261, :265
     meas = measurement_update_no(per, cfg, F)                           # :242-252
     slow = slow_time_signal(per)                                        # :257-260, :270
     fs = 1.0 / cfg.prt
     spec = eng.stft(slow, cfg.stft_window(), cfg.overlap, fs, nfft=0, n_log_bins=1024)   # :273-299
     spec = {"time": spec["time"].astype(np.float64), "frequency": spec["frequency"].astype(np.float64),
             "intensity": spec["intensity"].T.astype(np.float64), "nfft": spec["nfft"]}
-    paths = write_outputs_no(out_dir, filename, cfg, per, spec, meas, F, probe_col, per["probe_mag"], upload)
+    paths = write_outputs_no(out_dir, filename, cfg, per, spec, meas, F, probe_col,
+                             per["probe_mag"] if have_probe else None, upload)
     return {"paths": paths, "per_frame": per, "target_measurements": meas, "spectrogram": spec,
             "slow_time": slow}
 

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 1
+#define FMCW_ABI_VERSION 2
 
 typedef enum fmcw_status {
   FMCW_OK = 0,
@@ -83,9 +83,23 @@ int32_t     fmcw_abi_version(void);
 const char* fmcw_last_error(void);
 int         fmcw_device_count(int32_t* n);
 
-/* Bind a context to HIP device `device_id` (one stream, scratch, tables). */
-int fmcw_ctx_create(int32_t device_id, fmcw_ctx** out);
+/* Bind a context to n_devices HIP devices (device_ids[n_devices], or NULL for
+ * 0 .. n_devices-1), each with its own streams, scratch and tables, all in the
+ * calling process.  With several distinct devices the context also holds one
+ * RCCL communicator per device (ncclCommInitAll; RCCL is loaded
+ * at run time).  The host-pointer calls (fmcw_process, fmcw_range_fft,
+ * fmcw_stft) then split their work over the devices -- contiguous frame
+ * shards, each written back in place (the range_speed concatenation of
+ * :386-389 is the frame order), and contiguous spectrogram segment shards with
+ * the global max(P) of :282-283 taken by an RCCL all_reduce(max) -- so one MEX
+ * call from the serial loop's caller (radar_processing_with_azure.m:50 ->
+ * radar_processing.m:197) drives every GPU.  The device-pointer calls act on
+ * the first device (one process per GPU for torch.distributed drivers).
+ * Results do not depend on the number of devices (bit-identical shards). */
+int fmcw_ctx_create(int32_t n_devices, const int32_t* device_ids, fmcw_ctx** out);
 int fmcw_ctx_destroy(fmcw_ctx* ctx);
+/* n_devices, device_ids[n_devices] (may be NULL), rccl_comms: 1 if RCCL communicators exist. */
+int fmcw_ctx_devices(fmcw_ctx* ctx, int32_t* n_devices, int32_t* device_ids, int32_t* rccl_comms);
 
 /* Window taps and calibration (radar_processing.m:138, :139, :174):
  *   range_win   [nts]        = 2*blackman(NTS)
@@ -215,33 +229,20 @@ int fmcw_timing_reset(fmcw_ctx* ctx);
  * 0 restores the default. */
 int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
 
-/* Schedule of fmcw_process_device / fmcw_process (streams and fused give
- * identical bits; the single pass agrees with them to fp32 rounding):
+/* Schedule of fmcw_process_device / fmcw_process (the two agree to fp32 rounding):
  *  FMCW_PIPE_AUTO    the single pass where it applies (geometry below, no
- *                    range cube requested), else the streams schedule (at
- *                    2 MiB of fp32 range cube per frame the fused schedule
- *                    cannot keep its slots in L2 and is slower);
+ *                    range cube requested), else the streams schedule;
  *  FMCW_PIPE_STREAMS K1 | K2 | K3 kernels as a 3-stream chunk pipeline, the
  *                    range cube of each chunk round-trips through HBM;
- *  FMCW_PIPE_FUSED   one persistent kernel per call: each XCD runs its frames'
- *                    range, Doppler and detect items from a ticket queue, the
- *                    range cube of a frame stays in that XCD's L2.  E_ARG when
- *                    the geometry has no fused kernel or a cube is requested;
  *  FMCW_PIPE_ONEPASS single pass per frame (kernels_onepass.hip): 8 range tiles
  *                    per frame, each keeping its bins (r == t mod 8) of every
  *                    chirp in registers/LDS through the Doppler FFT, so the
  *                    range cube never reaches memory.  Needs nr 1024,
- *                    pn == nd == 256, even nts <= nr, complex64 in and out,
- *                    no range cube (else E_ARG).
- * nslot (>= 2, 0 = default 2): cube slots per XCD for the fused schedule. */
-enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_FUSED = 2, FMCW_PIPE_ONEPASS = 3 };
-int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode, int32_t nslot);
-
-/* Fused-schedule health after the last call (synchronises the stream):
- * 0 = every wait was satisfied, 1 = a bounded spin timed out (results of
- * that call are invalid; the call itself also returned FMCW_E_HIP when it
- * synchronised). */
-int fmcw_pipeline_status(fmcw_ctx* ctx, int32_t* status);
+ *                    pn == nd == 256, even nts <= nr, the RD map (if any) in the
+ *                    IQ dtype (complex64 or fp16 storage), no range cube (else E_ARG).
+ * (Value 2 is retired: the persistent "fused" schedule of ABI 1, slower than both.) */
+enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_ONEPASS = 3 };
+int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode);
 
 int fmcw_synchronize(fmcw_ctx* ctx);
 

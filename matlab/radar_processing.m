@@ -51,7 +51,11 @@ for f = 1:frame_count
     iq(:, :, f) = single(frame(f).Chirp(:, :, 1));
 end
 probe_col = 100;                         % reference :410
-[prof, cnt, ridx, rmag, didx, slow, probe] = fmcw_mex('process', P, iq, probe_col);
+% range_tx1rx1_complete(:,100) needs pn*frame_count >= 100 (reference :411); the
+% reference writes its first three JSON files before failing there, so the
+% probe is only requested when it exists and the error is raised at :411 below
+have_probe = pn * frame_count >= probe_col;
+[prof, cnt, ridx, rmag, didx, slow, probe] = fmcw_mex('process', P, iq, probe_col * have_probe);
 prof = double(prof); ridx = double(ridx); rmag = double(rmag); didx = double(didx);
 to_speed = @(d) (d - nd/2 - 1) * -fd_per_bin * lambda / 2;
 
@@ -79,6 +83,9 @@ if strcmpi(process_animal_activity, 'no')
          'array_bin_range', (0:nr-1) * dist_per_bin, 'range_tx1rx1_max_abs', prof, 'filename', filename));
     emit([filename, '_range_speed_data.json'], struct('time_axis', t_axis, ...
          'range', meas.range, 'speed', meas.speed, 'filename', filename));
+    if ~have_probe
+        error('MATLAB:badsubscript', 'Index in position 2 exceeds array bounds (must not exceed %d).', pn * frame_count);
+    end
     emit([filename, '_fft_data.json'], struct('range_bins', 0:nr-1, 'magnitude', double(probe), ...
          'frame_index', probe_col, 'filename', filename));
 

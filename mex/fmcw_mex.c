@@ -5,7 +5,9 @@
  * radar_processing(process_animal_activity) of the reference
  * (radar-etl-pipeline/radar_processing.m:56) and calls:
  *
- *   fmcw_mex('init', device_id)                                  -> fmcw_ctx_create (once; mexLock)
+ *   fmcw_mex('init', device_ids)                                 -> fmcw_ctx_create (once; mexLock);
+ *                                        device_ids: vector, default 0; several ids = one context over
+ *                                        several GPUs (frames and STFT segments sharded, RCCL max)
  *   fmcw_mex('taps', P, range_win, doppler_win, calib_rx1)       -> fmcw_set_taps       (:138-139, :174)
  *   [prof, cnt, ridx, rmag, didx, slow, probe] =
  *       fmcw_mex('process', P, iq, probe_column)                  -> fmcw_process        (:197-261, :265, :410)
@@ -88,8 +90,16 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
 
   if (!strcmp(cmd, "init")) {
     if (!g_ctx) {
-      const int dev = nrhs > 1 ? (int)mxGetScalar(prhs[1]) : 0;
-      check(fmcw_ctx_create(dev, &g_ctx));
+      int32_t ids[64] = {0};
+      int32_t n = 1;
+      if (nrhs > 1) {
+        const mxArray* a = prhs[1];
+        if (!mxIsDouble(a) || mxIsComplex(a) || mxGetNumberOfElements(a) < 1 || mxGetNumberOfElements(a) > 64)
+          mexErrMsgIdAndTxt("fmcw:arg", "init: device_ids must be a real double vector of 1..64 ids");
+        n = (int32_t)mxGetNumberOfElements(a);
+        for (int32_t i = 0; i < n; ++i) ids[i] = (int32_t)mxGetDoubles(a)[i];
+      }
+      check(fmcw_ctx_create(n, ids, &g_ctx));
       mexLock();
       mexAtExit(at_exit);
     }

@@ -22,6 +22,8 @@ int mxIsStruct(const mxArray* a);
 int mxIsNumeric(const mxArray* a);
 int mxIsSingle(const mxArray* a);
 int mxIsComplex(const mxArray* a);
+int mxIsDouble(const mxArray* a);
+double* mxGetDoubles(const mxArray* a);
 mwSize mxGetNumberOfElements(const mxArray* a);
 mwSize mxGetNumberOfDimensions(const mxArray* a);
 const mwSize* mxGetDimensions(const mxArray* a);

@@ -1,0 +1,114 @@
+"""GPU: one libfmcw context over several devices (include/fmcw.h fmcw_ctx_create
+with n_devices > 1) -- the path a single MEX call takes to drive every GPU of a
+node from the serial loop's caller (radar_processing_with_azure.m:50 ->
+radar_processing.m:197).
+
+The host-array calls shard frames (fmcw_process, fmcw_range_fft) and
+spectrogram segments (fmcw_stft) contiguously over the context's devices; the
+results must not depend on the number of devices, bit for bit.  On a one-GPU
+box several contexts share device 0 (the global max(P) then goes through the
+host: no RCCL communicator can span one device twice); with two or more GPUs
+the RCCL all_reduce path runs as well.
+"""
+import numpy as np
+import pytest
+
+from fmcw_radar_processing_amd import params as P
+from fmcw_radar_processing_amd.engine import Engine
+from oracle import oracle as O
+from tests.helpers import case
+
+pytestmark = pytest.mark.gpu
+
+
+def _n_gpus():
+    import torch
+    return torch.cuda.device_count()
+
+
+def _frames(F, geom, frame0=0):
+    nts, pn, nr, nd, mode = geom
+    cfg, p, wr, wd, cal = case(nts, pn, nr, nd, mode)
+    iq = O.synth_frames(F, pn, nts, nr, nd, p["dist_per_bin"], frame0=frame0)
+    return cfg, p, wr, wd, cal, iq
+
+
+GEOMS = [(1024, 256, 1024, 256, P.THROUGHPUT),   # single pass
+         (64, 16, 256, 16, P.PARITY)]            # deployed module, streams schedule
+
+
+@pytest.mark.parametrize("geom", GEOMS, ids=["cfg3", "deployed"])
+@pytest.mark.parametrize("ids", [[0], [0, 0], [0, 0, 0]])
+def test_sharded_process_is_bit_identical(engine, geom, ids):
+    F = 11 if geom[0] == 1024 else 40
+    cfg, p, wr, wd, cal, iq = _frames(F, geom, frame0=321)
+    engine.set_taps(cfg, cal, wr, wd)
+    probe = min(100 + geom[1] * (F // 2), F * geom[1])        # a column on the middle shard
+    ref = engine.process(iq, want_rd=True, probe_column=probe)
+    multi = Engine(ids)
+    try:
+        assert multi.device_info() == {"devices": ids, "rccl": False}
+        multi.set_taps(cfg, cal, wr, wd)
+        got = multi.process(iq, want_rd=True, probe_column=probe)
+    finally:
+        multi.close()
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+@pytest.mark.parametrize("ids", [[0, 0], [0, 0, 0, 0]])
+@pytest.mark.parametrize("nfft,nbins", [(0, 1024), (64, 0)])
+def test_sharded_stft_is_bit_identical(engine, ids, nfft, nbins):
+    cfg, p, wr, wd, cal = case(64, 16, 256, 16, P.PARITY)
+    rng = np.random.default_rng(5)
+    x = np.abs(rng.standard_normal(1333)).astype(np.float32) * 100
+    x[700:760] *= 50                                           # the global max sits on one shard
+    engine.set_taps(cfg, cal, wr, wd)
+    win = O.stft_window("kaiser")
+    ref = engine.stft(x, win, 19, 1 / p["prt"], nfft=nfft, n_log_bins=nbins)
+    multi = Engine(ids)
+    try:
+        multi.set_taps(cfg, cal, wr, wd)
+        got = multi.stft(x, win, 19, 1 / p["prt"], nfft=nfft, n_log_bins=nbins)
+    finally:
+        multi.close()
+    for k in ("time", "frequency", "intensity"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert got["nfft"] == ref["nfft"]
+
+
+def test_more_devices_than_frames(engine):
+    """Shards may be empty (F < devices): those devices sit the call out."""
+    cfg, p, wr, wd, cal, iq = _frames(2, GEOMS[1], frame0=9)
+    engine.set_taps(cfg, cal, wr, wd)
+    ref = engine.process(iq)
+    multi = Engine([0, 0, 0])
+    try:
+        multi.set_taps(cfg, cal, wr, wd)
+        got = multi.process(iq)
+    finally:
+        multi.close()
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+@pytest.mark.skipif(_n_gpus() < 2, reason="needs two GPUs (RCCL communicators over distinct devices)")
+def test_rccl_context_over_distinct_devices(engine):
+    n = _n_gpus()
+    cfg, p, wr, wd, cal, iq = _frames(2 * n + 1, GEOMS[0], frame0=77)
+    engine.set_taps(cfg, cal, wr, wd)
+    ref = engine.process(iq)
+    x = np.abs(np.random.default_rng(1).standard_normal(4000)).astype(np.float32)
+    win = O.stft_window("hann")
+    sref = engine.stft(x, win, 19, 1 / p["prt"], nfft=64, n_log_bins=0)
+    multi = Engine(list(range(n)))
+    try:
+        assert multi.device_info()["rccl"] is True
+        multi.set_taps(cfg, cal, wr, wd)
+        got = multi.process(iq)
+        sgot = multi.stft(x, win, 19, 1 / p["prt"], nfft=64, n_log_bins=0)
+    finally:
+        multi.close()
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    np.testing.assert_array_equal(sgot["intensity"], sref["intensity"])

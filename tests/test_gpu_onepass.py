@@ -27,7 +27,7 @@ def _frames(F, nts=1024, frame0=0):
 def onepass(engine):
     engine.set_pipeline(FMCW_PIPE_ONEPASS)
     yield engine
-    engine.set_pipeline(FMCW_PIPE_AUTO, 0)
+    engine.set_pipeline(FMCW_PIPE_AUTO)
     engine.set_chunk_frames(0)
 
 
@@ -185,47 +185,12 @@ def test_onepass_fp16_matches_streams_fp16(engine):
     engine.set_taps(cfg, cal, wr, wd)
     iq16 = np.stack([iq.real, iq.imag], -1).astype(np.float16)
     try:
-        engine.set_pipeline(FMCW_PIPE_AUTO, 0)
+        engine.set_pipeline(FMCW_PIPE_AUTO)
         a = _run_fp16(engine, iq16, F, 256)
         engine.set_pipeline(FMCW_PIPE_STREAMS)
         b = _run_fp16(engine, iq16, F, 256)
     finally:
-        engine.set_pipeline(FMCW_PIPE_AUTO, 0)
+        engine.set_pipeline(FMCW_PIPE_AUTO)
     assert (rel_l2(a["rd"].reshape(F, -1), b["rd"].reshape(F, -1), axis=1) <= TOL_FP16_REL_L2).all()
     for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-
-
-# Range pass variants of the single pass (kernels_onepass.hip): the pair
-# exchange (default), the same with the hand-off always released through
-# memory, with the partner's half always recomputed locally (the bounded-wait
-# fallback), and the 8-tile pass without exchange.
-_MODES = {"pair": {}, "release": {"FMCW_ONEPASS_XMODE": "1"}, "local": {"FMCW_ONEPASS_XMODE": "2"},
-          "tiles8": {"FMCW_ONEPASS_PAIR": "0"}}
-
-
-@pytest.mark.parametrize("mode", list(_MODES))
-def test_onepass_range_pass_modes(onepass, monkeypatch, mode):
-    for k, v in _MODES[mode].items():
-        monkeypatch.setenv(k, v)
-    cfg, p, wr, wd, cal, iq = _frames(21, frame0=500)
-    onepass.set_taps(cfg, cal, wr, wd)
-    got = onepass.process(iq, want_rd=True, probe_column=3000)
-    ref = O.process_frames(iq, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
-    _check_vs_oracle(cfg, got, ref, wd, 3000)
-
-
-def test_onepass_pair_handoff_is_exact(onepass, monkeypatch):
-    """The partner's half taken from the exchange buffer is bit-identical to the
-    same half recomputed locally (same arithmetic), whichever way it is published."""
-    cfg, p, wr, wd, cal, iq = _frames(19, nts=1000, frame0=77)
-    onepass.set_taps(cfg, cal, wr, wd)
-    out = {}
-    for mode in ("pair", "release", "local"):
-        monkeypatch.delenv("FMCW_ONEPASS_XMODE", raising=False)
-        for k, v in _MODES[mode].items():
-            monkeypatch.setenv(k, v)
-        out[mode] = onepass.process(iq, want_rd=True)
-    for mode in ("release", "local"):
-        for k in out["pair"]:
-            np.testing.assert_array_equal(out["pair"][k], out[mode][k], err_msg=f"{mode}:{k}")
