@@ -271,10 +271,7 @@ def cpu_baseline(budget_s: float, d_iq, F: int, dt: int):
     from fmcw_radar_processing_amd import params as P
     from oracle import coracle as CO
     from oracle import oracle as O
-    try:
-        cores = min(16, len(os.sched_getaffinity(0)))
-    except AttributeError:
-        cores = min(16, os.cpu_count() or 1)
+    cores, host = host_cores()
     cfg = P.config(4)
     p = O.derive_params(P.deployed_device(cfg.nts, cfg.pn), nr=cfg.nr, nd=cfg.nd, parity=False)
     wr, wd = O.windows(cfg.nts, cfg.pn)
@@ -310,7 +307,33 @@ def cpu_baseline(budget_s: float, d_iq, F: int, dt: int):
     return {"value": round(v_all, 2), "unit": "frames/s", "cores": cores, "kind": "port",
             "sample": f"{n_all} config-4 frames (the bench's own device frames, copied back) through "
                       f"oracle/fmcw_oracle.c (fp64, OpenMP {cores} threads, every RD row) + hop-1 STFT nfft 64",
-            "single_thread": {"value": round(v_one, 2), "frames": n_one}}
+            "single_thread": {"value": round(v_one, 2), "frames": n_one}, "host": host}
+
+
+def host_cores():
+    """Threads for the CPU baseline: every core this process may run on
+    (sched_getaffinity), bounded by the host's per-job share when the launcher
+    states one (OMP_NUM_THREADS; the GPU pool sets it to the cores it allots
+    to one GPU).  Returns (threads, description of the host)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    cores = min(aff, int(share)) if share.isdigit() and int(share) > 0 else aff
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    model = ln.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return cores, {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+                   "omp_num_threads_env": share or None,
+                   "threads_used": cores,
+                   "rule": "all affinity CPUs, bounded by OMP_NUM_THREADS when the launcher sets it"}
 
 
 if __name__ == "__main__":

@@ -645,6 +645,10 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
         lo = std::min(lo, h[8 * i]); hi = std::max(hi, h[8 * i + 5]);
         for (int q = 0; q < 5; ++q) ph[q] += (double)(h[8 * i + q + 1] - h[8 * i + q]);
       }
+      double w4 = 0, w7 = 0;   // range loop end of waves 4 and 7 (stamps 6, 7) after the prologue
+      for (size_t i = 0; i < nblk; ++i) { w4 += (double)(h[8 * i + 6] - h[8 * i + 1]); w7 += (double)(h[8 * i + 7] - h[8 * i + 1]); }
+      std::fprintf(stderr, "stamps-waves: range loop end after prologue (us): wave0 %.2f wave4 %.2f wave7 %.2f\n",
+                   ph[1] / nblk / 100.0, w4 / nblk / 100.0, w7 / nblk / 100.0);
       const double span = (double)(hi - lo);
       double life = 0;
       for (int q = 0; q < 5; ++q) life += ph[q];

@@ -94,6 +94,21 @@ __device__ __forceinline__ c2 cmul_a(c2 a, c2 b) {
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
   return r;
 }
+// 16-byte / 8-byte write-through store (global_store ... sc0 sc1): the line leaves the XCD's L2
+#ifdef OP_RD_PLAIN
+__device__ __forceinline__ void st_wt(f4v* p, f4v v) { *p = v; }
+__device__ __forceinline__ void st_wt(h4v* p, h4v v) { *p = v; }
+#else
+// The s_nop covers the store-data hazard the compiler cannot see through inline asm: a
+// VALU write to the data VGPRs of a > 8-byte VMEM store right after it needs wait states
+// (without it the next lane-pair exchange overwrote the data before the store read it).
+__device__ __forceinline__ void st_wt(f4v* p, f4v v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_wt(h4v* p, h4v v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+}
+#endif
 __device__ __forceinline__ c2 tov(float2 v) { return c2{v.x, v.y}; }
 __device__ __forceinline__ float2 tof(c2 v) { return make_float2(v.x, v.y); }
 __device__ __forceinline__ float abs2v(c2 v) { return fmaf(v.x, v.x, v.y * v.y); }
@@ -389,7 +404,11 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   // ---------------- range phase: :203-205 for chirps w + 8 k2 --------------
   // one load = one sample pair: 16 bytes (c64) or 8 bytes (c32h, half the L2 traffic)
   using TP = std::conditional_t<H, h4v, f4v>;
+#ifdef OP_XP_SAMEFR   // diagnostic: every tile of XCD x reads frame x (L2-resident input, no HBM stream)
+  const TP* __restrict__ fr = reinterpret_cast<const TP*>(a.iq) + (f & 7) * (int64_t)C * (S >> 1);
+#else
   const TP* __restrict__ fr = reinterpret_cast<const TP*>(a.iq) + f * (int64_t)C * (S >> 1);
+#endif
   const int S2 = S >> 1;                         // sample pairs per chirp
   const float ninvS = -1.0f / (float)S;
   auto ld_chirp = [&](int k, TP (&x)[8]) {
@@ -397,8 +416,12 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int p = lane + 64 * j;               // sample pair: samples 2p, 2p+1
+#ifdef OP_XP_NOLOAD  // diagnostic: no input loads (VALU-only range phase)
+      x[j] = __builtin_convertvector(f4v{(float)(lane + j), (float)k, (float)(p ^ k), 1.f}, TP);
+#else
       if constexpr (FULL) x[j] = (q + 64 * j)[lane];
       else x[j] = q[p < S2 ? p : 0];
+#endif
     }
   };
   auto widen = [&](const TP (&bf)[8], f4v (&x)[8]) {
@@ -441,12 +464,30 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     TP buf[RING][8];
 #pragma unroll
     for (int i = 0; i < RING - 1; ++i) ld_chirp(w + NW * ((i + rs) & (CPW - 1)), buf[i]);
+#ifdef OP_XP_DOPONLY  // diagnostic: no range phase (synthetic tile)
+#pragma unroll
+    for (int k2 = 0; k2 < CPW; ++k2) {
+      tile0[k2] = c2{(float)(lane * k2), (float)(w + k2)};
+      L.t1[(w + NW * k2) * 64 + lane] = c2{(float)(lane + k2), (float)(w * k2)};
+    }
+    if (0)
+#endif
 #pragma unroll
     for (int k2 = 0; k2 < CPW; ++k2) {
       const int k = w + NW * k2;                 // register order (chirp w + 8 ((k2 + rs) mod 32))
       if (k2 + RING - 1 < CPW) ld_chirp(w + NW * ((k2 + RING - 1 + rs) & (CPW - 1)), buf[(k2 + RING - 1) % RING]);
       f4v x[8];
       widen(buf[k2 % RING], x);
+#ifdef OP_XP_NOVALU  // diagnostic: the loads only (a plain sum keeps them live)
+      {
+        f4v s4 = x[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j) s4 += x[j];
+        tile0[k2] = s4.xy;
+        L.t1[k * 64 + lane] = s4.zw;
+        continue;
+      }
+#endif
       // stage A: sum_b x[a + 128 b] c_t[a + 128 b], straight from the loads
       c2 A0 = cmul_a(x[0].xy, cst[0]), A1 = cmul_a(x[0].zw, cst[1]);
       f4v s4 = x[0];
@@ -468,7 +509,21 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     }
   }
 
+#ifdef OP_XP_RANGEONLY  // diagnostic: stop after the range phase (one store keeps it live)
+  {
+    c2 acc = c2{0.f, 0.f};
+#pragma unroll
+    for (int k2 = 0; k2 < CPW; ++k2) acc += tile0[k2];
+    __syncthreads();
+    acc += L.t1[((w + 1) & 7) * 64 + lane];
+    a.profile[f * NR + (w * 64 + lane) % NR] = (acc.x + acc.y) * 0.f;   // 0 unless non-finite: no detections downstream
+    return;
+  }
+#endif
   // ---------------- per-row reductions over the 8 waves --------------------
+#ifdef OP_STAMPS
+  if (lane == 0 && (w == 4 || w == 7)) a.dbg[(int64_t)b * 8 + (w == 4 ? 6 : 7)] = __builtin_amdgcn_s_memrealtime();
+#endif
   stamp(2);
   __syncthreads();                               // B1: slot 1 complete in LDS
   c2 tile1[CPW];
@@ -616,8 +671,14 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
           const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
           const int e = (d2o & ~1) + CPW * (2 * m + (odd ? 1 : 0));
           const f4v o = odd ? f4v{rcv.x, rcv.y, B.x, B.y} : f4v{A.x, A.y, rcv.x, rcv.y};
-          if constexpr (H) out[e >> 1] = __builtin_convertvector(o * a.rd_scale, h4v);
-          else out[e >> 1] = o;
+#ifdef OP_XP_NOSTORE  // diagnostic: no RD stores (a never-taken store keeps the values live)
+          if (o.x == 1234.5f)
+#endif
+          // sc0 sc1: write-through stores that drop the line from the XCD's L2, so the RD map
+          // (never re-read by this kernel) does not evict input lines the other 7 tiles of the
+          // frame still read (measured +1.5 % over plain stores, 2 A/B rounds)
+          if constexpr (H) st_wt(out + (e >> 1), __builtin_convertvector(o * a.rd_scale, h4v));
+          else st_wt(out + (e >> 1), o);
         }
         continue;
       }
