@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-stage-timing", action="store_true")
     ap.add_argument("--no-fanout", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the extra single-GPU lines (fp16 storage, config 2, host-pointer path)")
     return ap.parse_args()
 
 
@@ -180,20 +182,18 @@ def main():
         path = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4), "unit": "GB/s",
                 "span_us": round(per_launch_ms * 1e3, 2), "frames_per_span": fpl, "alg_bytes_per_frame": alg_per_frame,
                 "what": "range+Doppler span (before first k_range .. after last k_doppler), SURVEY 8d bytes"}
-    pmc = load_pmc(os.path.join(ROOT, "profiles"), args)
+    pmc = load_pmc(os.path.join(ROOT, "profiles"))
     dom = "k_rd1p" if "k_rd1p" in kern else "k_range"
     if dom in kern:
         k = kern[dom]
-        traffic = None
-        if pmc and dom in pmc.get("kernels", {}):
-            pk = pmc["kernels"][dom]
-            if abs(pk.get("frames_per_launch", 0) - k["frames_per_launch"]) < 0.5:
-                traffic = pk.get("hbm_bytes_per_launch")
+        kname = RD1P_NAME[args.fp16] if dom == "k_rd1p" else None
+        traffic = pmc_traffic(pmc, kname, k["frames_per_launch"]) if kname else None
         roof = {"bound": "hbm", "achieved": k["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(k["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
                 "kernel": ("k_rd1p (single pass: calibration, mean removal, window, range FFT, profile, Doppler FFT, "
                            "RD store; one range tile of one frame per workgroup)") if dom == "k_rd1p" else
                           "k_range (K1: calibration, mean removal, window, 1024-pt range FFT, cube store)",
+                "kernel_name": RD1P_NAME[args.fp16] if dom == "k_rd1p" else None,
                 "alg_bytes_per_launch": k["alg_bytes_per_launch"], "avg_launch_us": k["avg_launch_us"],
                 "frames_per_launch": k["frames_per_launch"],
                 "traffic_source": pmc.get("source") if pmc and traffic else None}
@@ -217,6 +217,13 @@ def main():
                   "GBps_root_egress": round(world * nf * C * S * esz / ft / 1e9, 1)}
         del src, dst
 
+    extra = {}
+    if world == 1 and not args.no_extras and not args.fp16:
+        del d_rd, d_P
+        extra["fp16_storage"] = bench_fp16(eng, cfg, F, args, dev, stream, pmc)
+        extra["config2_range_fft"] = bench_config2(eng, args, dev, stream, pmc)
+        extra["host_path"] = bench_host_path(eng)
+        eng.set_taps(cfg, P.synth_calibration(S))
     if rank == 0:
         cpu = cpu_baseline(args.cpu_seconds, d_iq, F, dt) if args.cpu_seconds > 0 else None
         total_frames = world * F * args.steps
@@ -242,24 +249,186 @@ def main():
         }
         if fanout:
             line["input_fanout"] = fanout
+        line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def load_pmc(pdir: str, args):
-    """Per-launch HBM traffic of the dominant kernel from the committed rocprofv3
-    PMC summary of this same command (tools/profile_run.sh -> profiles/*pmc*.json):
+RD1P_NAME = {False: "fmcw::k_rd1p<true, false>", True: "fmcw::k_rd1p<true, true>"}
+K1_NAME = "fmcw::k_range<512, c64, c64, true>"
+
+
+def load_pmc(pdir: str):
+    """Per-launch HBM traffic per kernel from the committed rocprofv3 PMC summary
+    of this same command (tools/profile_run.sh -> profiles/bench_pmc.json):
     FETCH_SIZE x 2 (gfx950 read correction, MI355X_MICROARCH.md HBM section) +
-    WRITE_SIZE, averaged over the kernel's dispatches."""
-    name = "bench_fp16_pmc.json" if args.fp16 else "bench_pmc.json"
-    path = os.path.join(pdir, name)
+    WRITE_SIZE, averaged over the kernel's dispatches, keyed by kernel name."""
+    path = os.path.join(pdir, "bench_pmc.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
     d["source"] = os.path.relpath(path, ROOT)
     return d
+
+
+def pmc_traffic(pmc, name, frames_per_launch):
+    """HBM bytes per launch of kernel `name`, if the profile ran the same launch size."""
+    if not pmc:
+        return None
+    pk = (pmc.get("by_name") or {}).get(name)
+    if not pk or abs(pk.get("frames_per_launch", 0) - frames_per_launch) >= 0.5:
+        return None
+    return pk.get("hbm_bytes_per_launch")
+
+
+def _roof(alg_per_frame, frames_per_launch, avg_us, traffic, name, kernel, pmc):
+    ach = alg_per_frame * frames_per_launch / (avg_us * 1e-6) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": traffic, "kernel": kernel, "kernel_name": name,
+            "alg_bytes_per_launch": int(alg_per_frame * frames_per_launch), "avg_launch_us": round(avg_us, 2),
+            "frames_per_launch": frames_per_launch,
+            "traffic_source": pmc.get("source") if pmc and traffic else None}
+
+
+def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
+    """BASELINE config 4's fp16-storage variant, same step as the headline (fp16 IQ in,
+    fp16 RD map out, fp32 arithmetic), timed the same way on the same GPU."""
+    import torch
+    from fmcw_radar_processing_amd import FMCW_C32H
+    C, S, NR, ND = cfg.pn, cfg.nts, cfg.nr, cfg.nd
+    d_iq = torch.empty((F, C, S, 2), dtype=torch.float16, device=dev)
+    eng.synth_device(d_iq, 0, F, FMCW_C32H, stream=stream)
+    M = cfg.max_targets
+    outs = dict(profile=torch.empty((F, NR), device=dev), tgt_count=torch.empty(F, dtype=torch.int32, device=dev),
+                tgt_range_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
+                tgt_range_mag=torch.empty((F, M), device=dev),
+                tgt_doppler_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
+                slow_mag=torch.empty((F, C), device=dev))
+    d_rd = torch.empty((F, NR, ND, 2), dtype=torch.float16, device=dev)
+    win = torch.tensor(cfg.stft_window(), dtype=torch.float32, device=dev)
+    max_seg = F * C + STFT_WLEN - 1
+    flist = torch.empty(F, dtype=torch.int32, device=dev)
+    d_len = torch.zeros(1, dtype=torch.int64, device=dev)
+    d_P = torch.empty((max_seg, STFT_NFFT // 2 + 1), dtype=torch.float32, device=dev)
+    pmax = torch.zeros(1, dtype=torch.float32, device=dev)
+    nseg = torch.zeros(1, dtype=torch.int64, device=dev)
+    fs = 1.0 / cfg.prt
+
+    def step():
+        eng.process_device(d_iq, F, FMCW_C32H, outs, d_rd=d_rd, out_dtype=FMCW_C32H, stream=stream)
+        eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
+        pmax.zero_()
+        eng.stft_power_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
+                              max_seg, d_P, pmax, nseg, stream=stream)
+        eng.stft_db_device(d_P, nseg, max_seg, STFT_NFFT, fs, pmax, 0, d_P, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    eng.timing(2)
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    st = eng.timing_read()
+    eng.timing(0)
+    ms, n = st["onepass"]
+    fpl = F * args.steps / n
+    us = ms / n * 1e3
+    per = C * S * 4 + NR * ND * 4 + NR * 4
+    kname = RD1P_NAME[True]
+    out = {"value": round(F * args.steps / el, 1), "unit": "frames/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "dtype": "f16-storage/f32-compute",
+           "what": "BASELINE config 4 fp16-storage variant: the headline step with c32h IQ in and c32h RD out",
+           "roofline": _roof(per, fpl, us, pmc_traffic(pmc, kname, fpl), kname,
+                             "k_rd1p<fp16 storage> (single pass, c32h in / c32h RD out)", pmc)}
+    del d_iq, d_rd, d_P
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_config2(eng, args, dev, stream, pmc):
+    """BASELINE config 2: 4096 frames x 128 chirps x 512 samples, range FFT only (K1,
+    range cube written, fp32), device-resident; its own roofline on K1's event time."""
+    import torch
+    from fmcw_radar_processing_amd import FMCW_C64
+    from fmcw_radar_processing_amd import params as P
+    cfg2 = P.config(2)
+    F2, C, S, NR = 4096, cfg2.pn, cfg2.nts, cfg2.nr
+    eng.set_taps(cfg2, P.synth_calibration(S))
+    d_iq = torch.empty((F2, C, S, 2), dtype=torch.float32, device=dev)
+    eng.synth_device(d_iq, 0, F2, FMCW_C64, stream=stream)
+    d_cube = torch.empty((F2, C, NR, 2), dtype=torch.float32, device=dev)
+    d_prof = torch.empty((F2, NR), dtype=torch.float32, device=dev)
+    for _ in range(args.warmup):
+        eng.range_fft_device(d_iq, F2, FMCW_C64, d_cube, d_prof, stream=stream)
+    torch.cuda.synchronize(dev)
+    eng.timing(1)
+    eng.timing_reset()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.range_fft_device(d_iq, F2, FMCW_C64, d_cube, d_prof, stream=stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ms, n = eng.timing_read()["range_only"]
+    eng.timing(0)
+    us = ms / n * 1e3
+    per = C * S * 8 + C * NR * 8 + NR * 4
+    out = {"value": round(F2 * args.steps / el, 1), "unit": "frames/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "dtype": "f32", "what": "BASELINE config 2: 4096 x 128 x 512 IQ, range FFT only, cube + profile written",
+           "roofline": _roof(per, F2, us, pmc_traffic(pmc, K1_NAME, F2), K1_NAME,
+                             "K1 k_range (calibration, mean, window, 512-pt range FFT, cube + profile store)", pmc)}
+    del d_iq, d_cube, d_prof
+    torch.cuda.empty_cache()
+    return out
+
+
+def bench_host_path(eng):
+    """The path MATLAB calls (MEX -> fmcw_process + fmcw_stft on HOST buffers,
+    radar_processing.m:197-299): inputs in pageable host memory, PCIe included,
+    at the deployed 64x16 module geometry and at the config-3 geometry."""
+    import torch
+    from fmcw_radar_processing_amd import FMCW_C64
+    from fmcw_radar_processing_amd import params as P
+    from fmcw_radar_processing_amd import windows as W
+    res = {}
+    for name, F, reps in (("deployed_64x16", 16384, 5), ("config3_256x1024", 256, 3)):
+        cfg = P.config("deployed" if name.startswith("deployed") else 3)
+        eng.set_taps(cfg, P.synth_calibration(cfg.nts))
+        d = torch.empty((F, cfg.pn, cfg.nts, 2), dtype=torch.float32, device="cuda")
+        eng.synth_device(d, 0, F, FMCW_C64)                # SURVEY 8d frames, then to pageable host memory
+        torch.cuda.synchronize()
+        iq = d.cpu().numpy().view(np.complex64)[..., 0].copy()
+        del d
+        win = W.kaiser(20, 3.0)                            # :276 kaiser(window_length, 3)
+        fs = 1.0 / cfg.prt
+        out = eng.process(iq)                               # warm: slots allocated, code paged in
+        x = out["slow_mag"][out["tgt_count"] > 0].reshape(-1)
+        if len(x) < 20:
+            x = out["slow_mag"].reshape(-1)
+        eng.stft(x, win, 19, fs)
+        tp = ts = 0.0
+        for _ in range(reps):
+            t = time.perf_counter()
+            out = eng.process(iq)
+            tp += time.perf_counter() - t
+            x = out["slow_mag"][out["tgt_count"] > 0].reshape(-1)
+            if len(x) < 20:
+                x = out["slow_mag"].reshape(-1)
+            t = time.perf_counter()
+            eng.stft(x, win, 19, fs)                        # reference nfft rule + 1024 log bins (:270-299)
+            ts += time.perf_counter() - t
+        tp /= reps
+        ts /= reps
+        res[name] = {"frames": F, "frames_per_s": round(F / (tp + ts), 1), "process_ms": round(tp * 1e3, 3),
+                     "stft_ms": round(ts * 1e3, 3), "h2d_GBps": round(iq.nbytes / tp / 1e9, 2),
+                     "what": "fmcw_process (pageable host iq -> pinned 2-slot chunks -> HBM, outputs back) + "
+                             "fmcw_stft of the slow-time signal, wall clock"}
+    return res
 
 
 def cpu_baseline(budget_s: float, d_iq, F: int, dt: int):

@@ -70,6 +70,51 @@ struct DevBuf {
   ~DevBuf() { release(); }
 };
 
+// Page-locked host staging buffer (DMA source / target of the host-pointer calls).
+struct PinBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= n && p) return FMCW_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    n = 0;
+    if (bytes == 0) bytes = 16;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(FMCW_E_OOM, "hipHostMalloc of " + std::to_string(bytes) + " bytes failed");
+    }
+    n = bytes;
+    return FMCW_OK;
+  }
+  char* at(size_t off) const { return static_cast<char*>(p) + off; }
+  PinBuf() = default;
+  PinBuf(const PinBuf&) = delete;
+  PinBuf& operator=(const PinBuf&) = delete;
+  ~PinBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+
+// Host memcpy between the caller's (pageable) arrays and the pinned slots,
+// split over a few threads: one core copies ~10 GB/s, PCIe Gen5 x16 takes ~50.
+void par_memcpy(void* dst, const void* src, size_t n) {
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const unsigned T = n >= (8u << 20) ? std::min(8u, hw) : 1u;
+  if (T == 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  const size_t per = ((n + T - 1) / T + 4095) & ~(size_t)4095;
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t) {
+    const size_t o = (size_t)t * per;
+    if (o >= n) break;
+    th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, std::min(per, n - o)); });
+  }
+  for (auto& x : th) x.join();
+}
+
 size_t esize(int dtype) { return dtype == FMCW_C32H ? 4 : 8; }
 
 // RCCL, resolved at run time: a single-device context never needs it, and a
@@ -140,8 +185,14 @@ struct fmcw_ctx {
   float calw_scale = 0.f;
   float2 cal_sum{0.f, 0.f};
   DevBuf scratch_cube, scratch_rd;
-  // host-pointer API staging
-  DevBuf h_iq, h_prof, h_count, h_ridx, h_rmag, h_didx, h_slow, h_cube, h_rd, h_probe;
+  // host-pointer API staging: device slots and page-locked host slots, two of
+  // each, so chunk i+1's H2D copy (stream cin) and chunk i-1's D2H copy (cout)
+  // run under chunk i's kernels (the caller's data is copied into the pinned
+  // slots by host threads meanwhile)
+  DevBuf h_iq, h_prof, h_count, h_ridx, h_rmag, h_didx, h_slow, h_rd, h_probe;
+  PinBuf pin_in, pin_out;
+  hipStream_t cin = nullptr, cout = nullptr;
+  hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
@@ -176,9 +227,9 @@ struct fmcw_ctx {
     for (int i = 0; i < kSlots; ++i)
       for (hipEvent_t e : {ev_k1[i], ev_k2[i], ev_k3[i]})
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {ev_fork, ev_join})
+    for (hipEvent_t e : {ev_fork, ev_join, ev_h2d[0], ev_h2d[1], ev_comp[0], ev_comp[1], ev_d2h[0], ev_d2h[1]})
       if (e) (void)hipEventDestroy(e);
-    for (hipStream_t x : {sd, sx})
+    for (hipStream_t x : {sd, sx, cin, cout})
       if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -334,7 +385,12 @@ static int ctx_create_one(int32_t device_id, fmcw_ctx** out) {
   c->device = device_id;
   bool ok = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess &&
             hipStreamCreateWithFlags(&c->sd, hipStreamNonBlocking) == hipSuccess &&
-            hipStreamCreateWithFlags(&c->sx, hipStreamNonBlocking) == hipSuccess;
+            hipStreamCreateWithFlags(&c->sx, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->cin, hipStreamNonBlocking) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->cout, hipStreamNonBlocking) == hipSuccess;
+  for (int i = 0; i < 2; ++i)
+    for (hipEvent_t* e : {&c->ev_h2d[i], &c->ev_comp[i], &c->ev_d2h[i]})
+      ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   for (int i = 0; i < fmcw_ctx::kSlots; ++i)
     for (hipEvent_t* e : {&c->ev_k1[i], &c->ev_k2[i], &c->ev_k3[i]})
       ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
@@ -1069,6 +1125,94 @@ int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t 
 // ---------------------------------------------------------------------------
 // host-pointer per-frame API
 // ---------------------------------------------------------------------------
+}  // extern "C"
+
+// Frames per host-path chunk: ~64 MiB of input per slot (FMCW_HOST_CHUNK
+// overrides, for tests of the chunk seams).
+static int64_t host_chunk(size_t frame_in_bytes, int64_t F) {
+  int64_t fc = (int64_t)((64ull << 20) / std::max<size_t>(frame_in_bytes, 1));
+  if (const char* e = std::getenv("FMCW_HOST_CHUNK"); e && std::atoll(e) > 0) fc = std::atoll(e);
+  return std::max<int64_t>(1, std::min<int64_t>(fc, F));
+}
+
+// The host-pointer calls as a two-slot pipeline over chunks of frames:
+//   host:  caller's iq chunk i -> pinned slot i%2 (once the H2D of chunk i-2 has left it)
+//   cin:   pinned slot -> device slot (after chunk i-2's kernels released the device slot)
+//   s:     the device-pointer call on the chunk (small outputs written in place at f0)
+//   cout:  the chunk's large outputs (range cube, RD map) -> pinned out slot; the host
+//          copies chunk i-2's rows to the caller before that slot is reused
+// The small per-frame outputs stay on the device for all F and come back once.
+// `run(d_in, f0, nf, d_big[2])` enqueues the device call for one chunk on s.
+struct BigOut {
+  char* host;        // caller's [F][...] array or nullptr
+  size_t fbytes;     // bytes per frame
+};
+template <typename Run>
+static int host_pipeline(fmcw_ctx* c, const void* iq, int64_t F, size_t fin, const BigOut (&big)[2], Run&& run) {
+  hipStream_t s = c->stream;
+  const int64_t Fc = host_chunk(fin, F);
+  const size_t slot_in = (size_t)Fc * fin;
+  size_t slot_big[2], off_big[2] = {0, 0}, slot_out = 0;
+  bool any = false;
+  for (int q = 0; q < 2; ++q) {
+    slot_big[q] = big[q].host ? (size_t)Fc * big[q].fbytes : 0;
+    off_big[q] = slot_out;
+    slot_out += slot_big[q];
+    any = any || big[q].host;
+  }
+  CHK(c->h_iq.ensure(2 * slot_in));
+  CHK(c->pin_in.ensure(2 * slot_in));
+  if (any) {
+    CHK(c->h_rd.ensure(2 * slot_out));
+    CHK(c->pin_out.ensure(2 * slot_out));
+  }
+  const int64_t n = (F + Fc - 1) / Fc;
+  auto drain = [&](int64_t j) -> int {          // chunk j's large outputs: pinned slot -> caller
+    const int b = (int)(j & 1);
+    const int64_t f0 = j * Fc, nf = std::min(Fc, F - f0);
+    HIPCHK(hipEventSynchronize(c->ev_d2h[b]));
+    for (int q = 0; q < 2; ++q)
+      if (big[q].host)
+        par_memcpy(big[q].host + (size_t)f0 * big[q].fbytes, c->pin_out.at(b * slot_out + off_big[q]),
+                   (size_t)nf * big[q].fbytes);
+    return FMCW_OK;
+  };
+  HIPCHK(hipEventRecord(c->ev_fork, s));          // the device buffers are free once earlier work on s is done
+  HIPCHK(hipStreamWaitEvent(c->cin, c->ev_fork, 0));
+  for (int64_t i = 0; i < n; ++i) {
+    const int b = (int)(i & 1);
+    const int64_t f0 = i * Fc, nf = std::min(Fc, F - f0);
+    if (i >= 2) HIPCHK(hipEventSynchronize(c->ev_h2d[b]));   // pinned slot b: chunk i-2's H2D has read it
+    par_memcpy(c->pin_in.at(b * slot_in), static_cast<const char*>(iq) + (size_t)f0 * fin, (size_t)nf * fin);
+    if (i >= 2) HIPCHK(hipStreamWaitEvent(c->cin, c->ev_comp[b], 0));   // device slot b: chunk i-2's kernels are done
+    HIPCHK(hipMemcpyAsync(c->h_iq.as<char>() + b * slot_in, c->pin_in.at(b * slot_in), (size_t)nf * fin,
+                          hipMemcpyHostToDevice, c->cin));
+    HIPCHK(hipEventRecord(c->ev_h2d[b], c->cin));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_h2d[b], 0));
+    if (any && i >= 2) {                          // device out slot b: chunk i-2's D2H has read it
+      HIPCHK(hipStreamWaitEvent(s, c->ev_d2h[b], 0));
+      CHK(drain(i - 2));                          // and its rows go to the caller (pinned slot b is reused below)
+    }
+    char* d_big[2];
+    for (int q = 0; q < 2; ++q) d_big[q] = big[q].host ? c->h_rd.as<char>() + b * slot_out + off_big[q] : nullptr;
+    CHK(run(c->h_iq.as<char>() + b * slot_in, f0, nf, d_big));
+    HIPCHK(hipEventRecord(c->ev_comp[b], s));
+    if (any) {
+      HIPCHK(hipStreamWaitEvent(c->cout, c->ev_comp[b], 0));
+      for (int q = 0; q < 2; ++q)
+        if (big[q].host)
+          HIPCHK(hipMemcpyAsync(c->pin_out.at(b * slot_out + off_big[q]), d_big[q], (size_t)nf * big[q].fbytes,
+                                hipMemcpyDeviceToHost, c->cout));
+      HIPCHK(hipEventRecord(c->ev_d2h[b], c->cout));
+    }
+  }
+  if (any)
+    for (int64_t j = std::max<int64_t>(0, n - 2); j < n; ++j) CHK(drain(j));
+  return FMCW_OK;
+}
+
+extern "C" {
+
 static int process_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F,
                             float* prof, int32_t* count, int32_t* ridx, float* rmag, int32_t* didx, float* slow,
                             float* cube, float* rd, int64_t probe_column, float* probe) {
@@ -1079,31 +1223,32 @@ static int process_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, i
   if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
   const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
   hipStream_t s = c->stream;
-  CHK(c->h_iq.ensure((size_t)F * C * S * esize(in_dtype)));
   CHK(c->h_prof.ensure((size_t)F * NR * 4));
   CHK(c->h_count.ensure((size_t)F * 4));
   CHK(c->h_ridx.ensure((size_t)F * M * 4));
   CHK(c->h_rmag.ensure((size_t)F * M * 4));
   CHK(c->h_didx.ensure((size_t)F * M * 4));
   CHK(c->h_slow.ensure((size_t)F * C * 4));
-  if (cube) CHK(c->h_cube.ensure((size_t)F * C * NR * 8));
-  if (rd) CHK(c->h_rd.ensure((size_t)F * NR * ND * 8));
   if (probe) CHK(c->h_probe.ensure((size_t)NR * 4));
-  HIPCHK(hipMemcpyAsync(c->h_iq.p, iq, (size_t)F * C * S * esize(in_dtype), hipMemcpyHostToDevice, s));
-  CHK(fmcw_process_device(c, p, c->h_iq.p, in_dtype, F, c->h_prof.as<float>(), c->h_count.as<int32_t>(),
-                          c->h_ridx.as<int32_t>(), c->h_rmag.as<float>(), c->h_didx.as<int32_t>(), c->h_slow.as<float>(),
-                          cube ? c->h_cube.p : nullptr, rd ? c->h_rd.p : nullptr, FMCW_C64, probe ? probe_column : 0,
-                          probe ? c->h_probe.as<float>() : nullptr, s));
+  const size_t fin = (size_t)C * S * esize(in_dtype);
+  const BigOut big[2] = {{reinterpret_cast<char*>(cube), (size_t)C * NR * 8}, {reinterpret_cast<char*>(rd), (size_t)NR * ND * 8}};
+  CHK(host_pipeline(c, iq, F, fin, big, [&](char* d_in, int64_t f0, int64_t nf, char* const* d_big) {
+    const int64_t pc = probe && probe_column > f0 * C && probe_column <= (f0 + nf) * C ? probe_column - f0 * C : 0;
+    return fmcw_process_device(c, p, d_in, in_dtype, nf, c->h_prof.as<float>() + f0 * NR, c->h_count.as<int32_t>() + f0,
+                               c->h_ridx.as<int32_t>() + f0 * M, c->h_rmag.as<float>() + f0 * M,
+                               c->h_didx.as<int32_t>() + f0 * M, c->h_slow.as<float>() + f0 * C,
+                               d_big[0], d_big[1], FMCW_C64, pc,
+                               pc ? c->h_probe.as<float>() : nullptr, s);
+  }));
   HIPCHK(hipMemcpyAsync(prof, c->h_prof.p, (size_t)F * NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(count, c->h_count.p, (size_t)F * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(ridx, c->h_ridx.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(rmag, c->h_rmag.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(didx, c->h_didx.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipMemcpyAsync(slow, c->h_slow.p, (size_t)F * C * 4, hipMemcpyDeviceToHost, s));
-  if (cube) HIPCHK(hipMemcpyAsync(cube, c->h_cube.p, (size_t)F * C * NR * 8, hipMemcpyDeviceToHost, s));
-  if (rd) HIPCHK(hipMemcpyAsync(rd, c->h_rd.p, (size_t)F * NR * ND * 8, hipMemcpyDeviceToHost, s));
   if (probe) HIPCHK(hipMemcpyAsync(probe, c->h_probe.p, (size_t)NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipStreamSynchronize(c->cout));
   return FMCW_OK;
 }
 
@@ -1116,14 +1261,14 @@ static int range_fft_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq,
   if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
   const int S = p->nts, C = p->pn, NR = p->nr;
   hipStream_t s = c->stream;
-  CHK(c->h_iq.ensure((size_t)F * C * S * esize(in_dtype)));
-  CHK(c->h_cube.ensure((size_t)F * C * NR * 8));
   CHK(c->h_prof.ensure((size_t)F * NR * 4));
-  HIPCHK(hipMemcpyAsync(c->h_iq.p, iq, (size_t)F * C * S * esize(in_dtype), hipMemcpyHostToDevice, s));
-  CHK(fmcw_range_fft_device(c, p, c->h_iq.p, in_dtype, F, c->h_cube.p, FMCW_C64, c->h_prof.as<float>(), s));
-  HIPCHK(hipMemcpyAsync(cube, c->h_cube.p, (size_t)F * C * NR * 8, hipMemcpyDeviceToHost, s));
+  const BigOut big[2] = {{reinterpret_cast<char*>(cube), (size_t)C * NR * 8}, {nullptr, 0}};
+  CHK(host_pipeline(c, iq, F, (size_t)C * S * esize(in_dtype), big, [&](char* d_in, int64_t f0, int64_t nf, char* const* d_big) {
+    return fmcw_range_fft_device(c, p, d_in, in_dtype, nf, d_big[0], FMCW_C64, c->h_prof.as<float>() + f0 * NR, s);
+  }));
   HIPCHK(hipMemcpyAsync(prof, c->h_prof.p, (size_t)F * NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipStreamSynchronize(c->cout));
   return FMCW_OK;
 }
 

@@ -192,3 +192,14 @@ def test_fp16_storage_tolerance(engine):
     err = rd_rel_err(rd, ref["rd"], ref_c["cube"], wd, 256)
     assert err.max() <= TOL_FP16_REL_L2, err
     np.testing.assert_array_equal(outs["tgt_range_idx"].cpu().numpy(), ref["tgt_range_idx"])
+    # the STFT of the fp16-path slow-time rows (config 4: Hann(20), hop 1, nfft 64):
+    # fp16 storage bar |dB error| <= TOL_FP16_DB where psd > -60 dB
+    has = ref["tgt_count"] > 0
+    x = outs["slow_mag"].cpu().numpy()[has].reshape(-1).astype(np.float64)
+    xr = ref["slow_mag"][has].reshape(-1)
+    got = engine.stft(x, O.stft_window("hann"), 19, 1 / p["prt"], nfft=64, n_log_bins=0)
+    sp = O.spectrogram_pipeline(xr, p["prt"], O.stft_window("hann"), 19, nfft=64, nbins=0)
+    ri = sp["intensity"].T
+    sel = ri > -60
+    assert sel.sum() > 0
+    assert np.abs(got["intensity"][sel] - ri[sel]).max() <= TOL_FP16_DB

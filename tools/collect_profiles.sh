@@ -5,7 +5,7 @@ set -e
 tag=$1
 out=gpurun_out/prof_$tag
 js=profiles/bench_pmc.json
-[ "${2:-}" = "--fp16" ] && js=profiles/bench_fp16_pmc.json
+
 mkdir -p profiles
 python3 tools/pmc_summary.py $out --json $js --bench-log $out/stats.log > profiles/${tag}_summary.txt
 cp $out/stats/run_kernel_stats.csv profiles/${tag}_kernel_stats.csv

@@ -96,11 +96,30 @@ def main(d, json_out=None, bench_log=None):
             for line in open(bench_log):
                 if line.startswith("{") and '"metric"' in line:
                     bench = json.loads(line)
+        # every roofline object of the bench line names its kernel and launch size
+        roofs = {}
+        def walk(o):
+            if isinstance(o, dict):
+                if o.get("kernel_name") and "frames_per_launch" in o:
+                    roofs[o["kernel_name"]] = o
+                for v in o.values():
+                    walk(v)
+        walk(bench)
         out = {"prof_dir": d, "bench_line": {k: bench.get(k) for k in ("value", "ms_per_step", "dtype", "config")},
                "note": "hbm_bytes_per_launch = (2 x FETCH_SIZE + WRITE_SIZE) per dispatch; FETCH_SIZE x2 is the "
                        "gfx950 correction of MI355X_MICROARCH.md (HBM section); separate --pmc passes",
-               "kernels": {}}
+               "kernels": {}, "by_name": {}}
         for k, r in rows.items():
+            if "FETCH_SIZE" in r and "WRITE_SIZE" in r:
+                e = {"fetch_kib": round(r["FETCH_SIZE"], 1), "write_kib": round(r["WRITE_SIZE"], 1),
+                     "hbm_bytes_per_launch": int((2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024)}
+                if k in stat_us:
+                    e["rocprof_avg_us"], e["rocprof_calls"] = round(stat_us[k][0], 2), stat_us[k][1]
+                if k in roofs:
+                    e["frames_per_launch"] = roofs[k]["frames_per_launch"]
+                    e["bench_event_avg_us"] = roofs[k]["avg_launch_us"]
+                    e["alg_bytes_per_launch"] = roofs[k]["alg_bytes_per_launch"]
+                out["by_name"][k] = e
             lb = label(k)
             if not lb or "FETCH_SIZE" not in r or "WRITE_SIZE" not in r:
                 continue
