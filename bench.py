@@ -387,6 +387,27 @@ def bench_config2(eng, args, dev, stream, pmc):
     return out
 
 
+def json_timing(sp, python: bool):
+    """spectrogram_data.json (:306-321) of one call: libfmcw's native jsonencode writer
+    (SURVEY 8f #4) against the Python mirror of jsonencode, same bytes."""
+    import tempfile
+    from fmcw_radar_processing_amd import json_native
+    from fmcw_radar_processing_amd.matlab_json import encode
+    obj = {"time": sp["time"], "frequency": sp["frequency"], "intensity": sp["intensity"].T,
+           "title": "All Frames - Log-Scaled Spectrogram", "xLabel": "Time (s)", "yLabel": "Frequency (Hz)"}
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "spectrogram_data.json")
+        t = time.perf_counter()
+        n = json_native.write(path, obj)
+        out = {"native_ms": round((time.perf_counter() - t) * 1e3, 2)}
+        if python:
+            t = time.perf_counter()
+            with open(path, "w") as fh:
+                fh.write(encode(obj))
+            out["python_ms"] = round((time.perf_counter() - t) * 1e3, 2)
+    return out, n
+
+
 def bench_host_path(eng):
     """The path MATLAB calls (MEX -> fmcw_process + fmcw_stft on HOST buffers,
     radar_processing.m:197-299): inputs in pageable host memory, PCIe included,
@@ -426,7 +447,10 @@ def bench_host_path(eng):
             ts += time.perf_counter() - t
         tp /= reps
         ts /= reps
+        sp = eng.stft(x, win, 19, fs)
+        tj, nbytes = json_timing(sp, python=name.startswith("deployed"))
         res[name] = {"frames": F, "frames_per_s": round(F / (tp + ts), 1), "calls_per_s": round(1.0 / (tp + ts), 2),
+                     "spectrogram_json": {"bytes": nbytes, **tj},
                      "process_ms": round(tp * 1e3, 3),
                      "stft_ms": round(ts * 1e3, 3), "h2d_GBps": round(iq.nbytes / tp / 1e9, 2),
                      "what": "fmcw_process (pageable host iq -> pinned 2-slot chunks -> HBM, outputs back) + "

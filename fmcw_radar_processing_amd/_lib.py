@@ -38,6 +38,14 @@ class Params(ct.Structure):
     ]
 
 
+class JsonField(ct.Structure):
+    """fmcw_json_field (include/fmcw.h)."""
+    _fields_ = [("name", ct.c_char_p), ("kind", ct.c_int32), ("data", ct.c_void_p),
+                ("rows", ct.c_int64), ("cols", ct.c_int64), ("row_stride", ct.c_int64), ("col_stride", ct.c_int64)]
+
+
+FMCW_JSON_STRING, FMCW_JSON_F32, FMCW_JSON_F64, FMCW_JSON_I32 = 0, 1, 2, 3
+
 _P = ct.c_void_p
 _I32, _I64, _F, _D = ct.c_int32, ct.c_int64, ct.c_float, ct.c_double
 _PP = ct.POINTER(Params)
@@ -70,6 +78,7 @@ SIGNATURES = {
     "fmcw_set_chunk_frames": (ct.c_int, [_P, _I64]),
     "fmcw_set_pipeline": (ct.c_int, [_P, _I32]),
     "fmcw_synchronize": (ct.c_int, [_P]),
+    "fmcw_json_write": (ct.c_int, [ct.c_char_p, ct.POINTER(JsonField), _I32, _I32, _I32, ct.POINTER(_I64)]),
 }
 
 _lib = None

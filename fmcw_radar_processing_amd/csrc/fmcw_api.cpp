@@ -169,6 +169,10 @@ constexpr int kStages = 9;   // 0..6 per kernel (see fmcw.h), 7 range+Doppler sp
 
 }  // namespace
 
+namespace fmcw {
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace fmcw
+
 struct fmcw_ctx {
   int device = 0;
   hipStream_t stream = nullptr;

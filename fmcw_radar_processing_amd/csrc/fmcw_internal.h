@@ -197,4 +197,7 @@ hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s);
 bool range_size_supported(int nr);
 bool doppler_size_supported(int nd);
 
+// thread-local error text of fmcw_last_error (fmcw_api.cpp); returns code
+int set_error(int code, const char* msg);
+
 }  // namespace fmcw

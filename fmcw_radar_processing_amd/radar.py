@@ -16,8 +16,7 @@ driven, tested and benchmarked without MATLAB:
   :302-436  four JSON files + uploads                        -> write_outputs_no
   :440-607  'yes' branch: per-100-frame spectrogram JSONs     -> _run_yes
 
-Out of scope here: the spectrogram PNG (:331-348) and the blob
-uploads (``upload`` is a caller-supplied hook, default: none).
+The blob uploads are a caller-supplied hook (``upload``, default: none).
 """
 from __future__ import annotations
 
@@ -27,7 +26,8 @@ from typing import Callable
 import numpy as np
 
 from . import params as P
-from .matlab_json import encode, matlab_squeeze_2d
+from . import json_native
+from .matlab_json import matlab_squeeze_2d
 
 
 # ---------------------------------------------------------------------------
@@ -82,8 +82,9 @@ def slow_time_signal(per: dict, frames=None) -> np.ndarray:
 
 
 def write_json(path: str, obj: dict) -> str:
-    with open(path, "w") as fh:
-        fh.write(encode(obj, pretty=True))
+    """jsonencode(obj, 'PrettyPrint', true) + fprintf (:313-321 and friends) through
+    libfmcw's native writer (json_native; same bytes as matlab_json.encode)."""
+    json_native.write(path, obj, pretty=True)
     return path
 
 

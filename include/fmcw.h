@@ -246,6 +246,31 @@ int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode);
 
 int fmcw_synchronize(fmcw_ctx* ctx);
 
+/* ---------------------------------------------------------------------------
+ * Output files: native jsonencode(struct, 'PrettyPrint', true).
+ * Replaces the jsonencode + fprintf of radar_processing.m:313-321
+ * (spectrogram_data.json), :362-369 (<file>_range_fft_data.json), :390-398
+ * (<file>_range_speed_data.json), :424-431 (<file>_fft_data.json) and :590-593
+ * (the 'yes' branch's batch JSONs).  One field per struct member, in order:
+ *   FMCW_JSON_STRING  data = NUL-terminated char*, rows/cols ignored
+ *   FMCW_JSON_F32/F64/I32  a rows x cols MATLAB array; element (i, j) at
+ *     data[i * row_stride + j * col_stride] (so a [nseg][nbins] device-layout
+ *     intensity is written as MATLAB's nbins x nseg without a transpose).
+ * jsonencode's shape rules: 1x1 -> number, 1xN / Nx1 -> flat array, MxN ->
+ * array of M rows, empty -> []; NaN/Inf -> null; numbers as "%.15g" (integers
+ * without a fraction).  threads <= 0: up to 16 host threads format in parallel.
+ * No device work; no context needed.
+ * ------------------------------------------------------------------------- */
+enum { FMCW_JSON_STRING = 0, FMCW_JSON_F32 = 1, FMCW_JSON_F64 = 2, FMCW_JSON_I32 = 3 };
+typedef struct {
+  const char* name;
+  int32_t kind;
+  const void* data;
+  int64_t rows, cols, row_stride, col_stride;
+} fmcw_json_field;
+int fmcw_json_write(const char* path, const fmcw_json_field* fields, int32_t n_fields, int32_t pretty,
+                    int32_t threads, int64_t* bytes_written);
+
 #ifdef __cplusplus
 }
 #endif
