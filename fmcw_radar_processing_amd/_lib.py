@@ -19,7 +19,8 @@ FMCW_C64, FMCW_C32H = 0, 1
 FMCW_PIPE_AUTO, FMCW_PIPE_STREAMS, FMCW_PIPE_ONEPASS = 0, 1, 3
 ABI_VERSION = 2
 STATUS_NAMES = {0: "OK", -1: "E_ARG", -2: "E_HIP", -3: "E_OOM", -4: "E_STATE", -5: "E_DATA"}
-STAGES = ("range", "doppler", "detect", "compact", "stft_power", "stft_db", "range_only", "range_doppler", "onepass")
+STAGES = ("range", "doppler", "detect", "compact", "stft_power", "stft_db", "range_only", "range_doppler", "onepass",
+          "render")
 
 
 class FmcwError(RuntimeError):
@@ -79,6 +80,9 @@ SIGNATURES = {
     "fmcw_set_pipeline": (ct.c_int, [_P, _I32]),
     "fmcw_synchronize": (ct.c_int, [_P]),
     "fmcw_json_write": (ct.c_int, [ct.c_char_p, ct.POINTER(JsonField), _I32, _I32, _I32, ct.POINTER(_I64)]),
+    "fmcw_stft_png": (ct.c_int, [_P, _P, _I64, _P, _I32, _I32, _I32, _D, _I32, _P, _P, _P, ct.c_char_p, _I32, _I32,
+                                 ct.POINTER(_I64)]),
+    "fmcw_render_spectrogram_device": (ct.c_int, [_P, _P, _I32, _P, _P, _I32, _D, _D, _D, _I32, _I32, _P, _P]),
 }
 
 _lib = None

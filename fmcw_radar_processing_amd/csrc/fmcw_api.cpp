@@ -165,7 +165,7 @@ void shard(int64_t total, int g, int world, int64_t& f0, int64_t& n) {
   n = base + (g < rem ? 1 : 0);
 }
 
-constexpr int kStages = 9;   // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call, 8 k_rd1p
+constexpr int kStages = 10;  // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call, 8 k_rd1p, 9 render
 
 }  // namespace
 
@@ -198,6 +198,7 @@ struct fmcw_ctx {
   hipStream_t cin = nullptr, cout = nullptr;
   hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
+  DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
@@ -1028,8 +1029,48 @@ int fmcw_stft_sizes(int64_t L, int32_t wlen, int32_t noverlap, int32_t nfft, int
   return FMCW_OK;
 }
 
+int fmcw_render_spectrogram_device(fmcw_ctx* c, const float* d_Q, int32_t nq, const int64_t* d_nseg,
+                                   const float* d_pmax, int32_t nfft, double fs, double t0, double dt, int32_t width,
+                                   int32_t height, uint8_t* d_img, void* stream) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (!d_Q || !d_nseg || !d_pmax || !d_img) return fail(FMCW_E_ARG, "NULL device pointer");
+  if (nfft < 2 || (nfft % 2) != 0 || nq < 1 || nq > nfft / 2 || !(fs > 0) || !(dt > 0))
+    return fail(FMCW_E_ARG, "bad nfft / nq / fs / dt");
+  if (width < 1 || height < 1 || width > 65536 || height > 65535) return fail(FMCW_E_ARG, "bad image size");
+  CHK(set_device(c));
+  fmcw::RenderArgs a{};
+  a.Q = d_Q; a.nq = nq; a.nseg = d_nseg; a.pmax = d_pmax;
+  a.nb = nfft / 2 + 1; a.nfft = nfft; a.seam = a.nb - a.nb / 2 - 1;
+  a.fs = fs; a.t0 = t0; a.dt = dt;
+  a.fmax = FMCW_PNG_FMAX_HZ; a.cmin = FMCW_PNG_CMIN_DB; a.cmax = FMCW_PNG_CMAX_DB;
+  a.W = width; a.H = height; a.img = d_img;
+  hipStream_t s = pick(c, stream);
+  StageTimer tm(c, 9, s);
+  HIPCHK(fmcw::launch_render(a, s));
+  tm.done();
+  return FMCW_OK;
+}
+
+static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap,
+                     int32_t nfft, double fs, int32_t n_log_bins, float* T, float* freq, float* intensity,
+                     const char* png_path, int32_t width, int32_t height, int64_t* png_bytes);
+
 int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap, int32_t nfft,
               double fs, int32_t n_log_bins, float* T, float* freq, float* intensity) {
+  return stft_impl(c, x, L, win, wlen, noverlap, nfft, fs, n_log_bins, T, freq, intensity, nullptr, 0, 0, nullptr);
+}
+
+int fmcw_stft_png(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap,
+                  int32_t nfft, double fs, int32_t n_log_bins, float* T, float* freq, float* intensity,
+                  const char* png_path, int32_t width, int32_t height, int64_t* png_bytes) {
+  if (!png_path) return fail(FMCW_E_ARG, "png_path is NULL");
+  return stft_impl(c, x, L, win, wlen, noverlap, nfft, fs, n_log_bins, T, freq, intensity, png_path,
+                   width > 0 ? width : FMCW_PNG_DEFAULT_W, height > 0 ? height : FMCW_PNG_DEFAULT_H, png_bytes);
+}
+
+static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap,
+                     int32_t nfft, double fs, int32_t n_log_bins, float* T, float* freq, float* intensity,
+                     const char* png_path, int32_t width, int32_t height, int64_t* png_bytes) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   if ((!x && L > 0) || !win || !T || !freq || !intensity) return fail(FMCW_E_ARG, "NULL pointer");
   if (!(fs > 0)) return fail(FMCW_E_ARG, "fs must be > 0");
@@ -1096,6 +1137,41 @@ int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t 
       }
     }
   }
+  // 2b) spectrogram.png (:331-348) from the linear-bin P before it is overwritten:
+  //     the bins below ylim plus the Nyquist bin of every segment, gathered to device 0
+  std::vector<uint8_t> img;
+  if (png_path) {
+    const double df = fs / nf;
+    const int nq = (int)std::min<int64_t>(nb - 1, (int64_t)std::floor(FMCW_PNG_FMAX_HZ / df) + 2);
+    std::vector<float> q((size_t)std::max<int64_t>(nseg, 1) * (nq + 1));
+    for (int g = 0; g < world; ++g) {
+      fmcw_ctx* d = dev(g);
+      int64_t s0, ns;
+      shard(nseg, g, world, s0, ns);
+      if (ns == 0) continue;
+      CHK(set_device(d));
+      HIPCHK(hipMemcpy2DAsync(q.data() + s0 * (nq + 1), (nq + 1) * 4, d->s_P.p, (size_t)nb * 4, (size_t)nq * 4, ns,
+                              hipMemcpyDeviceToHost, d->stream));
+      HIPCHK(hipMemcpy2DAsync(q.data() + s0 * (nq + 1) + nq, (nq + 1) * 4, d->s_P.as<float>() + (nb - 1), (size_t)nb * 4,
+                              4, ns, hipMemcpyDeviceToHost, d->stream));
+    }
+    for (int g = 0; g < world; ++g) {
+      CHK(set_device(dev(g)));
+      HIPCHK(hipStreamSynchronize(dev(g)->stream));
+    }
+    CHK(set_device(c));
+    hipStream_t s = c->stream;
+    CHK(c->r_q.ensure(q.size() * 4));
+    CHK(c->r_nseg.ensure(8));
+    CHK(c->r_img.ensure((size_t)height * (width + 1)));
+    HIPCHK(hipMemcpyAsync(c->r_q.p, q.data(), q.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->r_nseg.p, &nseg, 8, hipMemcpyHostToDevice, s));
+    CHK(fmcw_render_spectrogram_device(c, c->r_q.as<float>(), nq, c->r_nseg.as<int64_t>(), c->s_pmax.as<float>(), nf, fs,
+                                       (wlen / 2.0) / fs, hop / fs, width, height, c->r_img.as<uint8_t>(), s));
+    img.resize((size_t)height * (width + 1));
+    HIPCHK(hipMemcpyAsync(img.data(), c->r_img.p, img.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+  }
   // 3) dB (+ log-frequency resampling) and the rows back into intensity
   for (int g = 0; g < world; ++g) {
     fmcw_ctx* d = dev(g);
@@ -1113,6 +1189,7 @@ int fmcw_stft(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t 
     CHK(set_device(dev(g)));
     HIPCHK(hipStreamSynchronize(dev(g)->stream));
   }
+  if (png_path) CHK(fmcw::png_write_indexed(png_path, img.data(), width, height, 1, 0, png_bytes));
   for (int64_t i = 0; i < nseg; ++i) T[i] = (float)(((double)i * hop + wlen / 2.0) / fs);   // spectrogram T
   if (n_log_bins > 0) {
     std::vector<int32_t> idx;

@@ -197,6 +197,24 @@ hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s);
 bool range_size_supported(int nr);
 bool doppler_size_supported(int nd);
 
+// spectrogram.png of :331-348 (kernels_render.hip)
+struct RenderArgs {
+  const float* Q;          // [nseg][nq + 1]: P of bins 0 .. nq-1, then the Nyquist bin nb-1
+  int nq;
+  const int64_t* nseg;     // device scalar
+  const float* pmax;       // device scalar: max(P(:)) (:282-283)
+  int nb, nfft, seam;      // one-sided bins, FFT size, the bin m whose face (m, m+1) fftshift drops
+  double fs, t0, dt;       // sample rate, T(1), T(2) - T(1)
+  double fmax, cmin, cmax; // ylim([0 fmax]), clim([cmin cmax])
+  int W, H;                // pixels
+  uint8_t* img;            // [H][1 + W] palette indices, PNG filter byte first
+};
+hipError_t launch_render(const RenderArgs& a, hipStream_t s);
+
+// png_writer.cpp: indexed PNG of [H][1 + W] rows (filter byte first), jet(256) palette
+int png_write_indexed(const char* path, const uint8_t* rows, int W, int H, int level, int threads, int64_t* bytes);
+void jet_palette(uint8_t* rgb);
+
 // thread-local error text of fmcw_last_error (fmcw_api.cpp); returns code
 int set_error(int code, const char* msg);
 

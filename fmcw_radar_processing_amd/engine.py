@@ -150,6 +150,27 @@ class Engine:
                                  int(n_log_bins), _ptr(T), _ptr(Fq), _ptr(inten)))
         return dict(time=T, frequency=Fq, intensity=inten, nfft=nf)
 
+    def stft_png(self, x: np.ndarray, win: np.ndarray, noverlap: int, fs: float, png_path: str, nfft: int = 0,
+                 n_log_bins: int = 1024, width: int = 0, height: int = 0) -> dict:
+        """:270-299 as ``stft`` plus spectrogram.png (:331-348) rendered on the device."""
+        x = np.ascontiguousarray(x, np.float32).reshape(-1)
+        w = np.ascontiguousarray(win, np.float32)
+        nseg, nf, nb = self.stft_sizes(len(x), len(w), noverlap, nfft, n_log_bins)
+        T = np.empty(nseg, np.float32)
+        Fq = np.empty(nb, np.float32)
+        inten = np.empty((nseg, nb), np.float32)
+        nbytes = ct.c_int64()
+        check(self.lib.fmcw_stft_png(self.h, _ptr(x), len(x), _ptr(w), len(w), int(noverlap), int(nfft), float(fs),
+                                     int(n_log_bins), _ptr(T), _ptr(Fq), _ptr(inten), str(png_path).encode(),
+                                     int(width), int(height), ct.byref(nbytes)))
+        return dict(time=T, frequency=Fq, intensity=inten, nfft=nf, png_bytes=nbytes.value)
+
+    def render_spectrogram_device(self, d_Q, nq: int, d_nseg, d_pmax, nfft: int, fs: float, t0: float, dt: float,
+                                  width: int, height: int, d_img, stream=None) -> None:
+        check(self.lib.fmcw_render_spectrogram_device(self.h, _ptr(d_Q), int(nq), _ptr(d_nseg), _ptr(d_pmax),
+                                                      int(nfft), float(fs), float(t0), float(dt), int(width),
+                                                      int(height), _ptr(d_img), _stream(stream)))
+
     # ---- device API (torch tensors as HBM buffers) -------------------------------
     def process_device(self, d_iq, F: int, in_dtype: int, outs: dict, d_cube=None, d_rd=None,
                        out_dtype: int = FMCW_C64, probe_column: int = 0, stream=None) -> None:

@@ -90,7 +90,7 @@ def write_json(path: str, obj: dict) -> str:
 
 def write_outputs_no(out_dir: str, filename: str, cfg: P.FmcwConfig, per: dict, spec: dict,
                      meas: dict, frame_count: int, probe_frame_index: int, probe_mag,
-                     upload: Callable[[str], None] | None = None) -> list:
+                     upload: Callable[[str], None] | None = None, png: str | None = None) -> list:
     """:302-436: the four JSON files of the 'no' branch, each uploaded right after
     it is written.  ``probe_mag`` None: the cube has fewer than ``probe_frame_index``
     columns, and -- as the reference at :411 -- the fourth file fails after the
@@ -108,6 +108,11 @@ def write_outputs_no(out_dir: str, filename: str, cfg: P.FmcwConfig, per: dict, 
         "time": spec["time"], "frequency": spec["frequency"],
         "intensity": spec["intensity"],                          # 1024 x nseg (bins down the rows)
         "title": "All Frames - Log-Scaled Spectrogram", "xLabel": "Time (s)", "yLabel": "Frequency (Hz)"}))
+    # :331-348 spectrogram.png (rendered by Engine.stft_png), then its upload (:347)
+    if png:
+        if upload:
+            upload(png)
+        paths.append(png)
     # :355-377 <filename>_range_fft_data.json
     time_axis = np.arange(frame_count) * 0.15
     paths.append(emit(os.path.join(out_dir, f"{filename}_range_fft_data.json"), {
@@ -170,11 +175,12 @@ def _run_no(eng, cfg, frames, F, filename, out_dir, upload):
     meas = measurement_update_no(per, cfg, F)                           # :242-252
     slow = slow_time_signal(per)                                        # :257-260, :270
     fs = 1.0 / cfg.prt
-    spec = eng.stft(slow, cfg.stft_window(), cfg.overlap, fs, nfft=0, n_log_bins=1024)   # :273-299
+    png = os.path.join(out_dir, "spectrogram.png")
+    spec = eng.stft_png(slow, cfg.stft_window(), cfg.overlap, fs, png, nfft=0, n_log_bins=1024)   # :273-299, :331-344
     spec = {"time": spec["time"].astype(np.float64), "frequency": spec["frequency"].astype(np.float64),
             "intensity": spec["intensity"].T.astype(np.float64), "nfft": spec["nfft"]}
     paths = write_outputs_no(out_dir, filename, cfg, per, spec, meas, F, probe_col,
-                             per["probe_mag"] if have_probe else None, upload)
+                             per["probe_mag"] if have_probe else None, upload, png=png)
     return {"paths": paths, "per_frame": per, "target_measurements": meas, "spectrogram": spec,
             "slow_time": slow}
 

@@ -219,7 +219,7 @@ int fmcw_synth_device(fmcw_ctx* ctx, const fmcw_params* p, int64_t frame0, int64
  * per STFT-side launch (stages 3-6); 2 = additionally one pair per K1/K2/K3.
  * stage: 0 range, 1 doppler, 2 detect, 3 compact, 4 stft_power, 5 stft_db,
  *        6 range_only, 7 range+Doppler span, 8 k_rd1p (single-pass schedule,
- *        level 2).  fmcw_timing_read synchronises. */
+ *        level 2), 9 render (spectrogram.png).  fmcw_timing_read synchronises. */
 int fmcw_timing_enable(fmcw_ctx* ctx, int32_t enable);
 int fmcw_timing_read(fmcw_ctx* ctx, int32_t stage, double* total_ms, int64_t* launches);
 int fmcw_timing_reset(fmcw_ctx* ctx);
@@ -245,6 +245,39 @@ enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_ONEPASS = 3 };
 int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode);
 
 int fmcw_synchronize(fmcw_ctx* ctx);
+
+/* ---------------------------------------------------------------------------
+ * spectrogram.png, replacing radar_processing.m:331-348:
+ *   surf(T, fftshift(F), fftshift(psd,1), 'EdgeColor','none'); view(0,90);
+ *   axis tight; ylim([0 150]); clim([-40 0]); axis off; colormap(jet);
+ *   exportgraphics(fig, 'spectrogram.png', 'Resolution', 600)
+ * rendered on the GPU (kernels_render.hip states the rules: the fftshift-ed
+ * one-sided axis folds the surface; the depth test of the top view; flat
+ * faces coloured by their first vertex through jet(256) on [-40 0] dB) and
+ * written as an 8-bit palette PNG.  Default size 2906 x 2038: the default
+ * axes box of a 600 x 400 figure (0.775 x 0.815 of it) at 600/96 px per
+ * screen pixel, which is what exportgraphics crops to with the axis off.
+ * MATLAB graphics cannot run here: the pixels are unpinned against it.
+ * ------------------------------------------------------------------------- */
+#define FMCW_PNG_FMAX_HZ 150.0
+#define FMCW_PNG_CMIN_DB (-40.0)
+#define FMCW_PNG_CMAX_DB 0.0
+#define FMCW_PNG_DEFAULT_W 2906
+#define FMCW_PNG_DEFAULT_H 2038
+
+/* fmcw_stft (:270-299) plus the PNG of :331-348 written to png_path
+ * (width/height 0: the defaults above); png_bytes may be NULL. */
+int fmcw_stft_png(fmcw_ctx* ctx, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap,
+                  int32_t nfft, double fs, int32_t n_log_bins, float* T, float* freq, float* intensity,
+                  const char* png_path, int32_t width, int32_t height, int64_t* png_bytes);
+
+/* Device call: palette indices img[height][1 + width] (PNG filter byte 0 first)
+ * from Q[nseg][nq + 1] = the one-sided P (:276) of bins 0 .. nq-1 followed by
+ * bin nfft/2 (for a full P row of nfft/2 + 1 bins: nq = nfft/2, Q = P), the
+ * global max(P) (:282), T(1) = t0, T(2) - T(1) = dt. */
+int fmcw_render_spectrogram_device(fmcw_ctx* ctx, const float* d_Q, int32_t nq, const int64_t* d_nseg,
+                                   const float* d_pmax, int32_t nfft, double fs, double t0, double dt, int32_t width,
+                                   int32_t height, uint8_t* d_img, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Output files: native jsonencode(struct, 'PrettyPrint', true).

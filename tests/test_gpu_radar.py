@@ -41,8 +41,11 @@ def test_radar_processing_no_branch(engine, tmp_path):
                              out_dir=str(tmp_path), engine=engine)
     p, per, meas, sp = _oracle_no(iq, nts, pn)
     names = sorted(os.listdir(tmp_path))
-    assert names == sorted(["spectrogram_data.json", "radar_data_range_fft_data.json",
+    assert names == sorted(["spectrogram_data.json", "spectrogram.png", "radar_data_range_fft_data.json",
                             "radar_data_range_speed_data.json", "radar_data_fft_data.json"])
+    from oracle import render as RR
+    img, pal = RR.read_png_indexed(str(tmp_path / "spectrogram.png"))   # :331-348 (tests/test_gpu_render.py)
+    assert img.shape == (2038, 2906) and len(np.unique(img)) > 10
     s = json.load(open(tmp_path / "spectrogram_data.json"))
     got = np.array(s["intensity"], dtype=np.float64)
     assert got.shape == sp["intensity"].shape
