@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--no-fanout", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the extra single-GPU lines (fp16 storage, config 2, host-pointer path)")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the host-pointer path line (profile runs: its small launches share kernel names)")
     return ap.parse_args()
 
 
@@ -222,7 +224,8 @@ def main():
         del d_rd, d_P
         extra["fp16_storage"] = bench_fp16(eng, cfg, F, args, dev, stream, pmc)
         extra["config2_range_fft"] = bench_config2(eng, args, dev, stream, pmc)
-        extra["host_path"] = bench_host_path(eng)
+        if not args.no_host_path:
+            extra["host_path"] = bench_host_path(eng)
         eng.set_taps(cfg, P.synth_calibration(S))
     if rank == 0:
         cpu = cpu_baseline(args.cpu_seconds, d_iq, F, dt) if args.cpu_seconds > 0 else None

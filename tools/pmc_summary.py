@@ -19,14 +19,38 @@ def short(name):
 
 
 def load_counters(path):
+    """Per kernel name, the dispatches of its LARGEST grid only (a kernel launched at
+    several sizes, e.g. k_rd1p for the 4096-frame step and for a small host-path
+    chunk, would otherwise average unlike launches)."""
+    rows = list(csv.DictReader(open(path)))
+    big = collections.defaultdict(int)
+    for r in rows:
+        k = short(r["Kernel_Name"])
+        big[k] = max(big[k], int(r["Grid_Size"]))
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     dur = collections.defaultdict(list)
-    with open(path) as fh:
-        for r in csv.DictReader(fh):
-            k = short(r["Kernel_Name"])
-            per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for r in rows:
+        k = short(r["Kernel_Name"])
+        if int(r["Grid_Size"]) != big[k]:
+            continue
+        per[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     return per, dur
+
+
+def trace_avg_us(path):
+    """(avg us, calls) per kernel name over the dispatches of its largest grid (kernel trace)."""
+    rows = list(csv.DictReader(open(path)))
+    big = collections.defaultdict(int)
+    for r in rows:
+        g = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        big[short(r["Kernel_Name"])] = max(big[short(r["Kernel_Name"])], g)
+    acc = collections.defaultdict(list)
+    for r in rows:
+        k = short(r["Kernel_Name"])
+        if int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]) == big[k]:
+            acc[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
 LABELS = ("k_range", "k_doppler", "k_detect_1p", "k_detect", "k_rd1p", "k_slow_fix", "k_rd_fused", "k_compact", "k_stft_power", "k_stft_db")
@@ -51,6 +75,9 @@ def main(d, json_out=None, bench_log=None):
                 stat_us[short(r['Name'])] = (float(r['AverageNs']) / 1e3, int(r['Calls']))
                 print(f"{short(r['Name']):72s} {int(r['Calls']):6d} {float(r['AverageNs'])/1e3:9.2f} "
                       f"{float(r['TotalDurationNs'])/1e6:9.2f} {float(r['Percentage']):6.2f}")
+    trace = os.path.join(d, "stats", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        stat_us.update(trace_avg_us(trace))        # per kernel: its largest launch only
     for sub in ("fetch", "write", "sq", "tcc", "sq2"):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
@@ -115,6 +142,7 @@ def main(d, json_out=None, bench_log=None):
                      "hbm_bytes_per_launch": int((2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024)}
                 if k in stat_us:
                     e["rocprof_avg_us"], e["rocprof_calls"] = round(stat_us[k][0], 2), stat_us[k][1]
+                    e["rocprof_avg_note"] = "kernel trace, dispatches of the kernel's largest grid"
                 if k in roofs:
                     e["frames_per_launch"] = roofs[k]["frames_per_launch"]
                     e["bench_event_avg_us"] = roofs[k]["avg_launch_us"]
