@@ -7,7 +7,8 @@ function radar_processing(process_animal_activity)
 %
 %   Host-side steps kept in MATLAB: parsing (:86), params (:89-154),
 %   calibration (:166-174), the measurement update with its (fr_idx, j)
-%   growth (:242-252) and the JSON / PNG / upload code (:302-436, :532-606).
+%   growth (:242-252) and the uploads; the JSON files and spectrogram.png are
+%   written by libfmcw (fmcw_mex 'json' / 'stft_png').
 
 addpath("lib");
 fdata = 'radar_data';
@@ -70,13 +71,13 @@ if strcmpi(process_animal_activity, 'no')
         end
     end
     iq_data = reshape(slow(:, cnt > 0), 1, []);          % :257-260, :270
-    [T, log_freq_bins, intensity] = fmcw_mex('stft', iq_data, single(kaiser(20, 3)), 19, 0, 1/prt, 1024);
-
+    % :270-299 and the spectrogram.png of :331-348, both from the one device STFT
+    [T, log_freq_bins, intensity] = fmcw_mex('stft_png', iq_data, single(kaiser(20, 3)), 19, 0, 1/prt, 1024, ...
+                                             'spectrogram.png');
     spec = struct('time', double(T), 'frequency', double(log_freq_bins), 'intensity', double(intensity), ...
                   'title', 'All Frames - Log-Scaled Spectrogram', 'xLabel', 'Time (s)', 'yLabel', 'Frequency (Hz)');
     emit('spectrogram_data.json', spec);
-    [T2, F2, psd2] = fmcw_mex('stft', iq_data, single(kaiser(20, 3)), 19, 0, 1/prt, 0);   % native bins, for the PNG
-    render_png(double(T2), double(F2), double(psd2));
+    send_picture_to_blob_storage('spectrogram.png');     % :347
 
     t_axis = (0:frame_count-1) * 0.15;
     emit([filename, '_range_fft_data.json'], struct('time_axis', t_axis, ...
@@ -114,23 +115,13 @@ end
 end
 
 function emit(name, s)
-% write one JSON file and upload it (reference :315-328 and friends)
-fid = fopen(name, 'w');
-if fid == -1
-    disp(['Error: Could not open ', name, ' for writing.']);
+% write one JSON file and upload it (reference :313-328 and friends): jsonencode(s,
+% 'PrettyPrint', true) + fprintf, natively in libfmcw (fmcw_json_write)
+try
+    fmcw_mex('json', name, s);
+catch err
+    disp(['Error: Could not write ', name, ': ', err.message]);
     return;
 end
-fprintf(fid, '%s', jsonencode(s, 'PrettyPrint', true));
-fclose(fid);
 send_json_string_to_blob_storage(name);
-end
-
-function render_png(T, F, psd)
-% spectrogram.png for the classifier (reference :331-348), from the native-bin psd
-fig = figure('Visible', 'off', 'Position', [100 100 600 400]);
-surf(T, fftshift(F), fftshift(psd, 1), 'EdgeColor', 'none');
-view(0, 90); axis tight; ylim([0 150]); clim([-40 0]); axis off; colormap(jet); colorbar('off');
-exportgraphics(fig, 'spectrogram.png', 'Resolution', 600);
-close(fig);
-send_picture_to_blob_storage('spectrogram.png');
 end

@@ -13,6 +13,12 @@
  *       fmcw_mex('process', P, iq, probe_column)                  -> fmcw_process        (:197-261, :265, :410)
  *   [T, freq, intensity] =
  *       fmcw_mex('stft', x, win, noverlap, nfft, fs, n_log_bins)  -> fmcw_stft           (:270-299)
+ *   [T, freq, intensity] =
+ *       fmcw_mex('stft_png', x, win, noverlap, nfft, fs, n_log_bins, png_path)
+ *                                                                 -> fmcw_stft_png  (:270-299 + :331-348)
+ *   bytes = fmcw_mex('json', path, s)                             -> fmcw_json_write (:313-321 and the other
+ *                                        jsonencode(s, 'PrettyPrint', true) + fprintf writes); s: a scalar
+ *                                        struct of char rows and double / single / int32 arrays
  *   fmcw_mex('close')                                             -> fmcw_ctx_destroy
  *
  * P is a struct with the fields of fmcw_params (nts, pn, nr, nd, max_targets,
@@ -109,6 +115,37 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (g_ctx) { fmcw_ctx_destroy(g_ctx); g_ctx = NULL; mexUnlock(); }
     return;
   }
+  if (!strcmp(cmd, "json")) {               /* bytes = fmcw_mex('json', path, s): needs no context */
+    if (nrhs != 3 || !mxIsChar(prhs[1]) || !mxIsStruct(prhs[2]) || mxGetNumberOfElements(prhs[2]) != 1)
+      mexErrMsgIdAndTxt("fmcw:arg", "json: path, scalar struct");
+    char path[4096];
+    if (mxGetString(prhs[1], path, sizeof path)) mexErrMsgIdAndTxt("fmcw:arg", "json: path too long");
+    const int nf = mxGetNumberOfFields(prhs[2]);
+    fmcw_json_field* fl = (fmcw_json_field*)mxCalloc(nf > 0 ? nf : 1, sizeof(fmcw_json_field));
+    for (int k = 0; k < nf; ++k) {
+      const mxArray* v = mxGetFieldByNumber(prhs[2], 0, k);
+      fl[k].name = mxGetFieldNameByNumber(prhs[2], k);
+      if (!v) mexErrMsgIdAndTxt("fmcw:arg", "json: field %s is empty", fl[k].name);
+      if (mxIsChar(v)) {
+        fl[k].kind = FMCW_JSON_STRING;
+        fl[k].data = mxArrayToUTF8String(v);          /* freed with the MEX call's memory */
+        continue;
+      }
+      if (mxIsComplex(v) || mxGetNumberOfDimensions(v) > 2)
+        mexErrMsgIdAndTxt("fmcw:arg", "json: field %s must be a real vector or matrix", fl[k].name);
+      fl[k].kind = mxIsDouble(v) ? FMCW_JSON_F64 : mxIsSingle(v) ? FMCW_JSON_F32 : mxIsInt32(v) ? FMCW_JSON_I32 : -1;
+      if (fl[k].kind < 0) mexErrMsgIdAndTxt("fmcw:arg", "json: field %s: double, single, int32 or char", fl[k].name);
+      fl[k].data = mxGetData(v);
+      fl[k].rows = (int64_t)mxGetM(v);
+      fl[k].cols = (int64_t)mxGetN(v);
+      fl[k].row_stride = 1;                          /* MATLAB column-major */
+      fl[k].col_stride = (int64_t)mxGetM(v);
+    }
+    int64_t bytes = 0;
+    check(fmcw_json_write(path, fl, nf, 1, 0, &bytes));
+    if (nlhs > 0) plhs[0] = mxCreateDoubleScalar((double)bytes);
+    return;
+  }
   if (!g_ctx) mexErrMsgIdAndTxt("fmcw:state", "call fmcw_mex('init') first");
 
   if (!strcmp(cmd, "taps")) {               /* fmcw_mex('taps', P, range_win, doppler_win, calib_rx1) */
@@ -146,8 +183,13 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     return;
   }
 
-  if (!strcmp(cmd, "stft")) {               /* fmcw_mex('stft', x, win, noverlap, nfft, fs, n_log_bins) */
-    if (nrhs != 7) mexErrMsgIdAndTxt("fmcw:arg", "stft: x, win, noverlap, nfft, fs, n_log_bins");
+  if (!strcmp(cmd, "stft") || !strcmp(cmd, "stft_png")) {
+    /* fmcw_mex('stft', x, win, noverlap, nfft, fs, n_log_bins [, png_path]) */
+    const int png = !strcmp(cmd, "stft_png");
+    if (nrhs != 7 + png) mexErrMsgIdAndTxt("fmcw:arg", "stft: x, win, noverlap, nfft, fs, n_log_bins[, png_path]");
+    char png_path[4096] = {0};
+    if (png && (!mxIsChar(prhs[7]) || mxGetString(prhs[7], png_path, sizeof png_path)))
+      mexErrMsgIdAndTxt("fmcw:arg", "stft_png: png_path must be a char row");
     const int64_t L = (int64_t)mxGetNumberOfElements(prhs[1]);
     const float* x = single_real(prhs[1], (mwSize)L, "x");
     const int32_t wlen = (int32_t)mxGetNumberOfElements(prhs[2]);
@@ -161,8 +203,12 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     plhs[0] = mxCreateNumericMatrix(1, nseg, mxSINGLE_CLASS, mxREAL);   /* T */
     plhs[1] = mxCreateNumericMatrix(1, nb, mxSINGLE_CLASS, mxREAL);     /* log_freq_bins / F */
     plhs[2] = mxCreateNumericMatrix(nb, nseg, mxSINGLE_CLASS, mxREAL);  /* interp_intensity */
-    check(fmcw_stft(g_ctx, x, L, w, wlen, nov, nfft, fs, nlog, mxGetSingles(plhs[0]), mxGetSingles(plhs[1]),
-                    mxGetSingles(plhs[2])));
+    if (png)
+      check(fmcw_stft_png(g_ctx, x, L, w, wlen, nov, nfft, fs, nlog, mxGetSingles(plhs[0]), mxGetSingles(plhs[1]),
+                          mxGetSingles(plhs[2]), png_path, 0, 0, NULL));
+    else
+      check(fmcw_stft(g_ctx, x, L, w, wlen, nov, nfft, fs, nlog, mxGetSingles(plhs[0]), mxGetSingles(plhs[1]),
+                      mxGetSingles(plhs[2])));
     return;
   }
   mexErrMsgIdAndTxt("fmcw:arg", "unknown command '%s'", cmd);

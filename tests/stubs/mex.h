@@ -31,4 +31,15 @@ float* mxGetSingles(const mxArray* a);
 int32_t* mxGetInt32s(const mxArray* a);
 mxComplexSingle* mxGetComplexSingles(const mxArray* a);
 mxArray* mxCreateNumericMatrix(mwSize m, mwSize n, mxClassID c, mxComplexity x);
+mxArray* mxCreateDoubleScalar(double v);
+int mxIsChar(const mxArray* a);
+int mxIsInt32(const mxArray* a);
+int mxGetNumberOfFields(const mxArray* s);
+mxArray* mxGetFieldByNumber(const mxArray* s, mwSize i, int k);
+const char* mxGetFieldNameByNumber(const mxArray* s, int k);
+char* mxArrayToUTF8String(const mxArray* a);
+void* mxGetData(const mxArray* a);
+mwSize mxGetM(const mxArray* a);
+mwSize mxGetN(const mxArray* a);
+void* mxCalloc(mwSize n, mwSize size);
 #endif
