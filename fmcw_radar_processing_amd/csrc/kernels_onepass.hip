@@ -610,92 +610,99 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     for (int k2 = 0; k2 < CPW; ++k2) x[k2] = (x[k2] - mu) * sload(a.wd, w + NW * ((k2 + rs) & (CPW - 1)));   // :218 (X - mean) .* 2chebwin
     dft32p(x);
   };
-  c2* stg = L.t1;                                // [wave][row lane][d2 ^ (lane & 31)]: conflict-free both ways
-  const int d2o = tid & 31;
-  c2 twr[NW];                                    // W256^(i d2o): the inter-stage twiddle, applied by the reader
+  // corner turn [wave][row][d2 ^ sw(row)], sw(row) = 2 (row mod 16): even, so a lane's d2
+  // pair (2q, 2q + 1) stays one aligned 16-byte word; conflict-free 8-byte writes
+  c2* stg = L.t1;
+  const int q2 = tid & 15;                       // the reader's d2 pair: 2 q2, 2 q2 + 1
+  // W256^((i + 8 rs) d2): the inter-stage twiddle W256^(i d2) times the W32^(rs d2) of the
+  // rotated registers (register r holds chirp group g = r + rs mod 32:
+  //   sum_g x_g W32^(g d2) = W32^(rs d2) sum_r x_(r + rs) W32^(r d2)), applied by the reader
+  c2 twr[2][NW];
 #pragma unroll
-  for (int i = 1; i < NW; ++i) twr[i] = tab[OP_TAB_TWR + i * 32 + d2o];
-  // rotated registers (register r holds chirp group g = r + rs mod 32):
-  //   sum_g x_g W32^(g d2) = W32^(rs d2) sum_r x_(r + rs) W32^(r d2),
-  // so each wave's DFT32 is multiplied by W32^(rs d2) = W256^(8 rs d2), folded into the
-  // reader's twiddle (wave 0 included)
-  if (rs) {
+  for (int e = 0; e < 2; ++e)
 #pragma unroll
-    for (int i = 0; i < NW; ++i) twr[i] = tab[OP_TAB_TWR2 + ((i + 8 * rs) & 255) * 32 + d2o];
-  }
-  // max / min over the 32 lanes of a row (DPP: xor 1, xor 2, then mirrors on
-  // group-uniform values, then the 16-lane row swap)
-  auto row_max = [&](int v) {
+    for (int i = 0; i < NW; ++i) twr[e][i] = tab[OP_TAB_TWR2 + ((i + 8 * rs) & 255) * 32 + 2 * q2 + e];
+  // max / min over the 16 lanes of a row (DPP: xor 1, xor 2, then mirrors on group-uniform values)
+  auto row_max16 = [&](int v) {
     v = max(v, dppi<0xB1>(v));
     v = max(v, dppi<0x4E>(v));
     v = max(v, dppi<0x141>(v));
-    v = max(v, dppi<0x140>(v));
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-    return max((int)r[0], (int)r[1]);
+    return max(v, dppi<0x140>(v));
   };
-  auto row_min = [&](int v) {
+  auto row_min16 = [&](int v) {
     v = min(v, dppi<0xB1>(v));
     v = min(v, dppi<0x4E>(v));
     v = min(v, dppi<0x141>(v));
-    v = min(v, dppi<0x140>(v));
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-    return min((int)r[0], (int)r[1]);
+    return min(v, dppi<0x140>(v));
   };
   auto stage = [&](const c2 (&z)[CPW]) {
 #pragma unroll
-    for (int d2 = 0; d2 < CPW; ++d2) stg[(w * 64 + lane) * CPW + (d2 ^ (lane & 31))] = z[d2];
+    for (int d2 = 0; d2 < CPW; ++d2) stg[(w * 64 + lane) * CPW + (d2 ^ ((lane & 15) << 1))] = z[d2];
   };
+  // Reader: 16 lanes per row, each with a d2 pair and all 8 d1, so it holds the two
+  // adjacent elements (2 q2, 2 q2 + 1) of every fftshift-ed column block: 16-byte stores
+  // with no lane exchange, 256 contiguous bytes per row and instruction
   auto post = [&](int sl) {
 #pragma unroll
-    for (int pass = 0; pass < 4; ++pass) {       // 16 rows per pass, 32 threads per row
-      const int lb = (tid >> 5) + 16 * pass;
-      c2 v[NW];
+    for (int pass = 0; pass < 2; ++pass) {       // 32 rows per pass
+      const int lb = (tid >> 4) + 32 * pass;
+      const int sw = (lb & 15) << 1;
+      c2 v0[NW], v1[NW];
 #pragma unroll
-      for (int i = 0; i < NW; ++i) v[i] = stg[(i * 64 + lb) * CPW + (d2o ^ (lb & 31))];
+      for (int i = 0; i < NW; ++i) {
+        const f4v pr = *reinterpret_cast<const f4v*>(&stg[(i * 64 + lb) * CPW + ((2 * q2) ^ sw)]);
+        v0[i] = pr.xy;
+        v1[i] = pr.zw;
+      }
 #pragma unroll
-      for (int i = 1; i < NW; ++i) v[i] = cmul_a(v[i], twr[i]);
-      if (rs) v[0] = cmul_a(v[0], twr[0]);
-      dft8p(v);
+      for (int i = 1; i < NW; ++i) {
+        v0[i] = cmul_a(v0[i], twr[0][i]);
+        v1[i] = cmul_a(v1[i], twr[1][i]);
+      }
+      if (rs) {
+        v0[0] = cmul_a(v0[0], twr[0][0]);
+        v1[0] = cmul_a(v1[0], twr[1][0]);
+      }
+      dft8p(v0);
+      dft8p(v1);
       const int r = t + 8 * lane_bin(lb) + 512 * sl;
-      // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element e = d2o + 32 d1s
+      // :219 fftshift(., 2): d1 -> position d1s = (d1 + 4) mod 8, element 2 q2 + e + 32 d1s
       if (a.rd) {                                // RD written: k_detect_1p reads the target rows' peaks from it
-        // 16-byte stores: lane pairs (d2o even / odd) swap one value per d1s pair,
-        // the even lane then writes elements (d2o, d2o + 1) of d1s = 2m, the odd
-        // lane those of d1s = 2m + 1: 512 contiguous bytes per row and instruction
         TP* __restrict__ out = reinterpret_cast<TP*>(a.rd) + (f * NR + r) * (int64_t)(ND / 2);
-        const bool odd = d2o & 1;
 #pragma unroll
-        for (int m = 0; m < NW / 2; ++m) {
-          const c2 A = v[(2 * m + NW / 2) & (NW - 1)], B = v[(2 * m + 1 + NW / 2) & (NW - 1)];
-          const c2 snd = odd ? A : B;
-          const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
-          const int e = (d2o & ~1) + CPW * (2 * m + (odd ? 1 : 0));
-          const f4v o = odd ? f4v{rcv.x, rcv.y, B.x, B.y} : f4v{A.x, A.y, rcv.x, rcv.y};
+        for (int d1s = 0; d1s < NW; ++d1s) {
+          const int d1 = (d1s + NW / 2) & (NW - 1);
+          const f4v o = f4v{v0[d1].x, v0[d1].y, v1[d1].x, v1[d1].y};
 #ifdef OP_XP_NOSTORE  // diagnostic: no RD stores (a never-taken store keeps the values live)
           if (o.x == 1234.5f)
 #endif
           // sc0 sc1: write-through stores that drop the line from the XCD's L2, so the RD map
           // (never re-read by this kernel) does not evict input lines the other 7 tiles of the
           // frame still read (measured +1.5 % over plain stores, 2 A/B rounds)
-          if constexpr (H) st_wt(out + (e >> 1), __builtin_convertvector(o * a.rd_scale, h4v));
-          else st_wt(out + (e >> 1), o);
+          if constexpr (H) st_wt(out + q2 + 16 * d1s, __builtin_convertvector(o * a.rd_scale, h4v));
+          else st_wt(out + q2 + 16 * d1s, o);
         }
         continue;
       }
       // :233 [val, di] = max(abs(.)): exact max of |D|^2 over the row, then its first index
-      float q[NW];
+      float qa[NW], qb[NW];
 #pragma unroll
-      for (int d1s = 0; d1s < NW; ++d1s) q[d1s] = abs2v(v[(d1s + NW / 2) & (NW - 1)]);
-      float m = q[0];
+      for (int d1s = 0; d1s < NW; ++d1s) {
+        qa[d1s] = abs2v(v0[(d1s + NW / 2) & (NW - 1)]);
+        qb[d1s] = abs2v(v1[(d1s + NW / 2) & (NW - 1)]);
+      }
+      float m = fmaxf(qa[0], qb[0]);
 #pragma unroll
-      for (int d1s = 1; d1s < NW; ++d1s) m = fmaxf(m, q[d1s]);
-      const float rm = __int_as_float(row_max(__float_as_int(m)));   // non-negative: int order == float order
+      for (int d1s = 1; d1s < NW; ++d1s) m = fmaxf(m, fmaxf(qa[d1s], qb[d1s]));
+      const float rm = __int_as_float(row_max16(__float_as_int(m)));   // non-negative: int order == float order
       int e = INT_MAX;
 #pragma unroll
-      for (int d1s = NW - 1; d1s >= 0; --d1s)
-        if (q[d1s] == rm) e = d2o + CPW * d1s;
-      e = row_min(e);
-      if (d2o == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
+      for (int d1s = NW - 1; d1s >= 0; --d1s) {
+        if (qb[d1s] == rm) e = 2 * q2 + 1 + CPW * d1s;
+        if (qa[d1s] == rm) e = 2 * q2 + CPW * d1s;
+      }
+      e = row_min16(e);
+      if (q2 == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
     }
   };
   pre(tile0, mu0);
