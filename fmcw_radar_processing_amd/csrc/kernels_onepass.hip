@@ -113,6 +113,20 @@ __device__ __forceinline__ c2 tov(float2 v) { return c2{v.x, v.y}; }
 __device__ __forceinline__ float2 tof(c2 v) { return make_float2(v.x, v.y); }
 __device__ __forceinline__ float abs2v(c2 v) { return fmaf(v.x, v.x, v.y * v.y); }
 __device__ __forceinline__ c2 mnegi(c2 a) { return c2{a.y, -a.x}; }   // a * (-i)
+// a + (-i) b = (a.re + b.im, a.im - b.re) and a + i b = (a.re - b.im, a.im + b.re) as ONE
+// v_pk_add_f32 (op_sel swaps b's halves, neg_* flips one of them): the compiler would
+// build the rotated b with moves and sign flips first.  Not fed to DPP/permlane (the
+// Doppler DFTs only): no hazard the compiler cannot see.
+__device__ __forceinline__ c2 add_mi(c2 a, c2 b) {
+  c2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ c2 add_pi(c2 a, c2 b) {
+  c2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 
 // DPP lane read; old = 0 with bound_ctrl lets the compiler fuse the move
 // into the consuming VOP2 (v_add_f32_dpp, v_max_u32_dpp, ...).
@@ -256,11 +270,19 @@ __device__ __forceinline__ c2 wave_sum_c(c2 s) {
 
 // ---- packed small DFTs (natural order in and out) ------------------------
 __device__ __forceinline__ void dft4p(c2& a0, c2& a1, c2& a2, c2& a3) {
-  const c2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = mnegi(a1 - a3);
+  const c2 t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, d = a1 - a3;
   a0 = t0 + t2;
   a2 = t0 - t2;
-  a1 = t1 + t3;
-  a3 = t1 - t3;
+  a1 = add_mi(t1, d);                            // t1 + (-i) d
+  a3 = add_pi(t1, d);                            // t1 - (-i) d
+}
+// the same with a2 entering as (-i) a2 (the W16^4 twiddle of dft16p folded in)
+__device__ __forceinline__ void dft4p_m2(c2& a0, c2& a1, c2& a2, c2& a3) {
+  const c2 t0 = add_mi(a0, a2), t1 = add_pi(a0, a2), t2 = a1 + a3, d = a1 - a3;
+  a0 = t0 + t2;
+  a2 = t0 - t2;
+  a1 = add_mi(t1, d);
+  a3 = add_pi(t1, d);
 }
 constexpr float kH = 0.70710678118654752440f;
 __device__ __forceinline__ void dft8p(c2 (&v)[8]) {
@@ -268,12 +290,11 @@ __device__ __forceinline__ void dft8p(c2 (&v)[8]) {
   c2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
   dft4p(e0, e1, e2, e3);
   dft4p(o0, o1, o2, o3);
-  o1 = c2{o1.x + o1.y, o1.y - o1.x} * kH;       // * W8^1 = h(1 - i)
-  o2 = mnegi(o2);                                // * W8^2 = -i
-  o3 = c2{o3.y - o3.x, -(o3.x + o3.y)} * kH;    // * W8^3 = h(-1 - i)
+  o1 = add_mi(o1, o1) * kH;                     // * W8^1 = h(1 - i): h (re + im, im - re)
+  o3 = add_pi(o3, o3) * -kH;                     // * W8^3 = h(-1 - i): -h (re - im, im + re)
   v[0] = e0 + o0; v[4] = e0 - o0;
   v[1] = e1 + o1; v[5] = e1 - o1;
-  v[2] = e2 + o2; v[6] = e2 - o2;
+  v[2] = add_mi(e2, o2); v[6] = add_pi(e2, o2);  // * W8^2 = -i folded into the butterfly
   v[3] = e3 + o3; v[7] = e3 - o3;
 }
 // 16 points: X[k1 + 4 k2] = sum_n2 W4^(n2 k2) W16^(n2 k1) sum_n1 x[4 n1 + n2] W4^(n1 k1)
@@ -291,7 +312,7 @@ __device__ __forceinline__ void dft16p(c2* v) {
   y[6] = cmv(y[6], c2{kH, -kH});
   y[7] = cmv(y[7], c2{s1, -c1});
   y[9] = cmv(y[9], c2{kH, -kH});
-  y[10] = mnegi(y[10]);
+  // y[10] * W16^4 = -i: folded into the k1 = 2 column's DFT4 (dft4p_m2)
   y[11] = cmv(y[11], c2{-kH, -kH});
   y[13] = cmv(y[13], c2{s1, -c1});
   y[14] = cmv(y[14], c2{-kH, -kH});
@@ -299,7 +320,8 @@ __device__ __forceinline__ void dft16p(c2* v) {
 #pragma unroll
   for (int k1 = 0; k1 < 4; ++k1) {
     c2 a0 = y[k1], a1 = y[4 + k1], a2 = y[8 + k1], a3 = y[12 + k1];
-    dft4p(a0, a1, a2, a3);
+    if (k1 == 2) dft4p_m2(a0, a1, a2, a3);
+    else dft4p(a0, a1, a2, a3);
     v[STRIDE * k1] = a0; v[STRIDE * (k1 + 4)] = a1; v[STRIDE * (k1 + 8)] = a2; v[STRIDE * (k1 + 12)] = a3;
   }
 }
@@ -321,7 +343,12 @@ __device__ __forceinline__ void dft32p(c2 (&v)[32]) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const c2 e = v[2 * k];
-    const c2 ot = k == 0 ? v[1] : (k == 8 ? mnegi(v[17]) : cmv(v[2 * k + 1], c2{kc[k], -ks[k]}));   // W32^k O[k]
+    if (k == 8) {                                // W32^8 O[8] = -i O[8]
+      r[k] = add_mi(e, v[17]);
+      r[k + 16] = add_pi(e, v[17]);
+      continue;
+    }
+    const c2 ot = k == 0 ? v[1] : cmv(v[2 * k + 1], c2{kc[k], -ks[k]});   // W32^k O[k]
     r[k] = e + ot;
     r[k + 16] = e - ot;
   }
