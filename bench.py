@@ -113,12 +113,16 @@ def main():
             head = fdist.head_samples(outs["slow_mag"], flist, d_len, h)
             hbuf, hl = fdist.right_halo(head, lens, rank)
         pmax.zero_()
+        # two-pass STFT without a stored P: pass 1 forms max(P) only, pass 2 recomputes P and
+        # writes 20 log10(P / max) (:276-283) -- P never goes to HBM and back
         eng.stft_power_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
-                              max_seg, d_P, pmax, nseg, d_halo=hbuf, n_halo=h if world > 1 else 0,
+                              max_seg, None, pmax, nseg, d_halo=hbuf, n_halo=h if world > 1 else 0,
                               d_halo_len=hl, stream=stream)
         if world > 1:
             fdist.global_max_(pmax)
-        eng.stft_db_device(d_P, nseg, max_seg, STFT_NFFT, fs, pmax, 0, d_P, stream=stream)
+        eng.stft_db_direct_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
+                                  max_seg, pmax, d_P, d_halo=hbuf, n_halo=h if world > 1 else 0, d_halo_len=hl,
+                                  stream=stream)
         if world > 1:
             fdist.gather_range_speed(outs["tgt_count"], outs["tgt_range_idx"], outs["tgt_doppler_idx"],
                                      outs["tgt_range_mag"])
@@ -324,8 +328,9 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
         eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
         pmax.zero_()
         eng.stft_power_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
-                              max_seg, d_P, pmax, nseg, stream=stream)
-        eng.stft_db_device(d_P, nseg, max_seg, STFT_NFFT, fs, pmax, 0, d_P, stream=stream)
+                              max_seg, None, pmax, nseg, stream=stream)
+        eng.stft_db_direct_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
+                                  max_seg, pmax, d_P, stream=stream)
 
     for _ in range(args.warmup):
         step()

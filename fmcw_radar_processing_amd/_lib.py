@@ -72,6 +72,8 @@ SIGNATURES = {
     "fmcw_stft_power_device": (ct.c_int, [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I32, _I32, _I32, _D, _I64,
                                           _P, _P, _P, _P]),
     "fmcw_stft_db_device": (ct.c_int, [_P, _P, _P, _I64, _I32, _D, _P, _I32, _P, _P]),
+    "fmcw_stft_db_direct_device": (ct.c_int, [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I32, _I32, _I32, _D, _I64,
+                                              _P, _P, _P]),
     "fmcw_synth_device": (ct.c_int, [_P, _PP, _I64, _I64, _P, _I32, _P]),
     "fmcw_timing_enable": (ct.c_int, [_P, _I32]),
     "fmcw_timing_read": (ct.c_int, [_P, _I32, ct.POINTER(_D), ct.POINTER(_I64)]),

@@ -199,6 +199,7 @@ struct fmcw_ctx {
   hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
+  DevBuf s_tab;                                // STFT 20-tap table W[nfft/2+1][20]
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
@@ -936,8 +937,8 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   CHK(check_stft_shape(wlen, noverlap, nfft));
   if (pn < 1 || n_halo < 0 || max_seg < 0 || !(fs > 0)) return fail(FMCW_E_ARG, "bad pn / n_halo / max_seg / fs");
-  if (!d_slow || !d_list || !d_len || !d_win || !d_P || !d_pmax || !d_nseg || (n_halo > 0 && !d_halo))
-    return fail(FMCW_E_ARG, "NULL device pointer");
+  if (!d_slow || !d_list || !d_len || !d_win || !d_pmax || !d_nseg || (n_halo > 0 && !d_halo))
+    return fail(FMCW_E_ARG, "NULL device pointer");   // d_P may be NULL: max(P) only
   // the shard split of the slow-time signal (dist.py) starts every shard's segment grid at its own
   // sample 0 and takes wlen-1 samples of right halo: that is the global grid only for hop 1
   if (n_halo > 0 && wlen - noverlap != 1)
@@ -951,7 +952,42 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
   a.inv_fs = (float)(1.0 / fs);
   a.max_seg = max_seg; a.P = d_P; a.pmax = d_pmax; a.nseg_out = d_nseg;
   StageTimer tm(c, 4, s);
-  HIPCHK(fmcw::launch_stft_power(a, s));
+  if (fmcw::stft_fast_path(wlen, a.hop)) {        // the reference's 20-tap window: W table + k_stft20
+    CHK(c->s_tab.ensure((size_t)(nfft / 2 + 1) * 20 * 8));
+    HIPCHK(fmcw::launch_stft_table(d_win, nfft, c->s_tab.as<float2>(), s));
+    HIPCHK(fmcw::launch_stft20(a, c->s_tab.as<float2>(), d_P ? 0 : 1, nullptr, s));
+  } else {
+    HIPCHK(fmcw::launch_stft_power(a, s));
+  }
+  tm.done();
+  return FMCW_OK;
+}
+
+int fmcw_stft_db_direct_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_list, const int64_t* d_len,
+                               int32_t pn, const float* d_halo, int32_t n_halo, const int64_t* d_halo_len,
+                               const float* d_win, int32_t wlen, int32_t noverlap, int32_t nfft, double fs,
+                               int64_t max_seg, const float* d_pmax, float* d_out, void* stream) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  CHK(check_stft_shape(wlen, noverlap, nfft));
+  if (pn < 1 || n_halo < 0 || max_seg < 0 || !(fs > 0)) return fail(FMCW_E_ARG, "bad pn / n_halo / max_seg / fs");
+  if (!d_slow || !d_list || !d_len || !d_win || !d_pmax || !d_out || (n_halo > 0 && !d_halo))
+    return fail(FMCW_E_ARG, "NULL device pointer");
+  if (!fmcw::stft_fast_path(wlen, wlen - noverlap))
+    return fail(FMCW_E_ARG, "the direct dB STFT needs the 20-tap window and hop <= 4");
+  if (n_halo > 0 && wlen - noverlap != 1)
+    return fail(FMCW_E_ARG, "a halo (sharded STFT) needs hop 1, i.e. noverlap = wlen - 1");
+  CHK(set_device(c));
+  hipStream_t s = pick(c, stream);
+  fmcw::StftArgs a{};
+  a.slow_mag = d_slow; a.frame_list = d_list; a.len = d_len; a.pn = pn;
+  a.halo = d_halo; a.n_halo = n_halo; a.halo_len = d_halo_len;
+  a.win = d_win; a.wlen = wlen; a.hop = wlen - noverlap; a.nfft = nfft;
+  a.inv_fs = (float)(1.0 / fs);
+  a.max_seg = max_seg; a.P = nullptr; a.pmax = const_cast<float*>(d_pmax); a.nseg_out = nullptr;
+  StageTimer tm(c, 5, s);
+  CHK(c->s_tab.ensure((size_t)(nfft / 2 + 1) * 20 * 8));
+  HIPCHK(fmcw::launch_stft_table(d_win, nfft, c->s_tab.as<float2>(), s));
+  HIPCHK(fmcw::launch_stft20(a, c->s_tab.as<float2>(), 2, d_out, s));
   tm.done();
   return FMCW_OK;
 }

@@ -162,6 +162,12 @@ struct StftArgs {
   int64_t* nseg_out;
 };
 
+// 20-tap fast path (kernels_stft.hip k_stft20): W table [nfft/2+1][20] from the window,
+// then mode 0 P + max, 1 max only, 2 dB written to dst (given max)
+bool stft_fast_path(int wlen, int hop);
+hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_t s);
+hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s);
+
 struct StftDbArgs {
   const float* P;
   const int64_t* nseg;

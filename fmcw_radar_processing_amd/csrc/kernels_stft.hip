@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
     }
     const float k = (bin == 0 || 2 * bin == a.nfft) ? 1.f : 2.f;  // one-sided 'psd'
     const float p = cabs2(acc) * p_scale * k;
-    a.P[(s0 + sl) * nb + bin] = p;
+    if (a.P) a.P[(s0 + sl) * nb + bin] = p;
     lmax = fmaxf(lmax, p);
   }
 #pragma unroll
@@ -119,6 +119,113 @@ __global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
   if (threadIdx.x == 0) {
     const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
     atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+  }
+}
+
+// ---------------------------------------------------------------------------
+// STFT fast path for the reference's 20-tap window (:276 kaiser(20,3); config 4
+// Hann(20)).  One thread per segment, 256 segments per workgroup:
+//   S(seg, bin) = sum_m x[seg hop + m] * W[bin][m],  W[bin][m] = w[m] e^{-2 pi i bin m/nfft}
+// x[0..19] in registers; W read as wave-uniform scalar loads (every lane of a
+// wave evaluates the same bin), so each complex MAC of a real sample is two
+// v_fma_f32 with an SGPR operand -- no per-output sincos, no Horner chain, no
+// 64-bit division.  Output tiles of 256 segments x 32 bins go through LDS so the
+// stores are coalesced.  MODE 0: P (one-sided 'psd') + max(P); MODE 1: max(P)
+// only; MODE 2: psd = 20 log10(P / max) (:283) written directly (the P of a
+// second pass, recomputed instead of stored and re-read).
+// ---------------------------------------------------------------------------
+constexpr int STFT_W = 20;
+
+__global__ __launch_bounds__(256) void k_stft_table(const float* __restrict__ win, int nfft, float2* __restrict__ tab) {
+  const int nb = nfft / 2 + 1;
+  const int64_t n = (int64_t)nb * STFT_W;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int k = (int)(i / STFT_W), m = (int)(i - (int64_t)k * STFT_W);
+    double sn, cs;
+    sincospi(2.0 * (double)((int64_t)k * m % nfft) / (double)nfft, &sn, &cs);   // exact phase reduction, fp64
+    tab[i] = make_float2((float)(win[m] * cs), (float)(-win[m] * sn));
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __restrict__ tab, float* __restrict__ dst) {
+  constexpr int TS = 256, KC = 32;
+  __shared__ float xs[TS * 4 + STFT_W];         // hop <= 4 (the reference's is 1): 38 KiB of LDS, 4 blocks per CU
+  __shared__ float tile[TS][KC + 1];
+  __shared__ float bmax[4];
+  const int64_t L = *a.len;
+  const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
+  const int64_t Lx = L + H;
+  const int noverlap = STFT_W - a.hop;
+  int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
+  if (nseg > a.max_seg) nseg = a.max_seg;
+  if (MODE != 2 && blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+  const int64_t s0 = (int64_t)blockIdx.x * TS;
+  if (s0 >= nseg) return;                                           // block-uniform
+  const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
+  const int nsamp = (ns - 1) * a.hop + STFT_W;
+  const int64_t q0 = s0 * a.hop;
+  for (int i = threadIdx.x; i < nsamp; i += 256) {
+    const int64_t q = q0 + i;
+    xs[i] = q < L ? a.slow_mag[(int64_t)a.frame_list[q / a.pn] * a.pn + (q % a.pn)] : a.halo[q - L];
+  }
+  __syncthreads();
+  const int sl = threadIdx.x;
+  const bool valid = sl < ns;
+  float x[STFT_W];
+#pragma unroll
+  for (int m = 0; m < STFT_W; ++m) x[m] = valid ? xs[sl * a.hop + m] : 0.f;
+  typedef float f2t __attribute__((ext_vector_type(2)));
+  const __attribute__((address_space(4))) f2t* T = (const __attribute__((address_space(4))) f2t*)(const void*)tab;
+  float u = 0.f;                                                    // sum(w.^2): |W[0][m]|^2
+#pragma unroll
+  for (int m = 0; m < STFT_W; ++m) u = fmaf(T[m].x, T[m].x, u);
+  const float scale = a.inv_fs / u;                                 // 1/(fs*sum(w.^2))
+  float inv = 0.f;
+  if constexpr (MODE == 2) {
+    const float pm = *a.pmax;
+    inv = pm > 0.f ? 1.0f / pm : 0.f;                               // all-zero P: -Inf dB (MATLAB G = 0)
+  }
+  const int nb = a.nfft / 2 + 1;
+  float lmax = 0.f;
+  for (int k0 = 0; k0 < nb; k0 += KC) {                             // uniform: bins k0 .. k0+KC-1
+    const int kn = nb - k0 < KC ? nb - k0 : KC;
+#pragma unroll 4
+    for (int kk = 0; kk < kn; ++kk) {             // unrolled: the scalar table loads of 4 bins issue together
+      const int k = k0 + kk;
+      const auto* Wk = T + (int64_t)k * STFT_W;
+      float re = 0.f, im = 0.f;
+#pragma unroll
+      for (int m = 0; m < STFT_W; ++m) {
+        const f2t wk = Wk[m];
+        re = fmaf(x[m], wk.x, re);
+        im = fmaf(x[m], wk.y, im);
+      }
+      const float g = (k == 0 || 2 * k == a.nfft) ? 1.f : 2.f;     // one-sided 'psd'
+      const float p = fmaf(re, re, im * im) * scale * g;
+      if (valid) lmax = fmaxf(lmax, p);
+      if constexpr (MODE == 0) tile[sl][kk] = p;
+      if constexpr (MODE == 2) tile[sl][kk] = 20.0f * log10f(p * inv);
+    }
+    if constexpr (MODE != 1) {
+      __syncthreads();
+      float* out = MODE == 0 ? a.P : dst;
+      for (int i = threadIdx.x; i < ns * kn; i += 256) {            // row-major [seg][bin] chunk, coalesced per row
+        const int r = i / kn, c = i - r * kn;
+        out[(s0 + r) * nb + k0 + c] = tile[r][c];
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (MODE != 2) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    if ((threadIdx.x & 63) == 0) bmax[threadIdx.x >> 6] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
+      atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+    }
   }
 }
 
@@ -221,6 +328,25 @@ static unsigned grid_for(int64_t n, int per_thread = 1) {
 
 hipError_t launch_compact(const int32_t* count, int64_t F, int pn, int32_t* list, int64_t* len, hipStream_t s) {
   hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, count, F, pn, list, len);
+  return hipGetLastError();
+}
+
+bool stft_fast_path(int wlen, int hop) { return wlen == STFT_W && hop >= 1 && hop <= 4; }
+
+hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_t s) {
+  const int64_t n = (int64_t)(nfft / 2 + 1) * STFT_W;
+  hipLaunchKernelGGL(k_stft_table, dim3(grid_for(n)), dim3(256), 0, s, win, nfft, tab);
+  return hipGetLastError();
+}
+
+hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s) {
+  if (a.max_seg <= 0) return hipSuccess;
+  if (!stft_fast_path(a.wlen, a.hop)) return hipErrorInvalidValue;
+  const int64_t blocks = (a.max_seg + 255) / 256;
+  if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+  else if (mode == 1) hipLaunchKernelGGL(k_stft20<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+  else hipLaunchKernelGGL(k_stft20<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
   return hipGetLastError();
 }
 

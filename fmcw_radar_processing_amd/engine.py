@@ -201,6 +201,14 @@ class Engine:
                                               int(nfft), float(fs), int(max_seg), _ptr(d_P), _ptr(d_pmax),
                                               _ptr(d_nseg), _stream(stream)))
 
+    def stft_db_direct_device(self, d_slow, d_list, d_len, pn: int, d_win, wlen: int, noverlap: int, nfft: int,
+                              fs: float, max_seg: int, d_pmax, d_out, d_halo=None, n_halo: int = 0, d_halo_len=None,
+                              stream=None) -> None:
+        check(self.lib.fmcw_stft_db_direct_device(self.h, _ptr(d_slow), _ptr(d_list), _ptr(d_len), int(pn),
+                                                  _ptr(d_halo), int(n_halo), _ptr(d_halo_len), _ptr(d_win),
+                                                  int(wlen), int(noverlap), int(nfft), float(fs), int(max_seg),
+                                                  _ptr(d_pmax), _ptr(d_out), _stream(stream)))
+
     def stft_db_device(self, d_P, d_nseg, max_seg: int, nfft: int, fs: float, d_pmax, n_log_bins: int, d_out,
                        stream=None) -> None:
         check(self.lib.fmcw_stft_db_device(self.h, _ptr(d_P), _ptr(d_nseg), int(max_seg), int(nfft), float(fs),

@@ -190,7 +190,7 @@ int fmcw_compact_device(fmcw_ctx* ctx, const int32_t* d_tgt_count, int64_t F, in
  * H = *d_halo_len when d_halo_len != NULL (device int64, <= n_halo), else
  * n_halo.  The halo carries the first samples of the following shards in the
  * multi-GPU split of the concatenated slow-time signal (:259).
- *   d_P [max_seg][nfft/2+1]  MATLAB P (psd scaling, one-sided)
+ *   d_P [max_seg][nfft/2+1]  MATLAB P (psd scaling, one-sided); NULL: only max(P) is formed
  *   d_pmax                   running max of P (float, atomically raised;
  *                            initialise to 0 before the first call)
  *   d_nseg                   int64 device: segments actually written */
@@ -206,6 +206,17 @@ int fmcw_stft_power_device(fmcw_ctx* ctx, const float* d_slow_mag, const int32_t
 int fmcw_stft_db_device(fmcw_ctx* ctx, const float* d_P, const int64_t* d_nseg, int64_t max_seg,
                         int32_t nfft, double fs, const float* d_pmax, int32_t n_log_bins,
                         float* d_out, void* stream);
+
+/* Second pass of the two-pass STFT without a stored P (20-tap window, hop <= 4,
+ * linear bins only): recomputes P of every segment and writes
+ * psd = 20*log10(P / max) (:283) to d_out [max_seg][nfft/2+1].  With
+ * fmcw_stft_power_device(..., d_P = NULL, ...) as the first pass (max(P) only)
+ * the P map is never written to or read back from HBM.  Same inputs as the power
+ * call; d_pmax is the (all-reduced) max. */
+int fmcw_stft_db_direct_device(fmcw_ctx* ctx, const float* d_slow, const int32_t* d_list, const int64_t* d_len,
+                               int32_t pn, const float* d_halo, int32_t n_halo, const int64_t* d_halo_len,
+                               const float* d_win, int32_t wlen, int32_t noverlap, int32_t nfft, double fs,
+                               int64_t max_seg, const float* d_pmax, float* d_out, void* stream);
 
 /* Synthetic IQ frames of SURVEY 8d (seed 0xF3C0 ^ global frame index),
  * generated in place in HBM: d_iq [F][pn][nts] of dtype.  Bench input only. */

@@ -1,6 +1,7 @@
 """GPU parity of the device-pointer path that bench.py times (BASELINE config 4):
 
   process_device -> compact_device -> stft_power_device -> stft_db_device
+  (and bench.py's form: stft_power_device with no P -> stft_db_direct_device)
 
 over many config-3/4 frames, some without a target, against the float64
 oracle on the same inputs: the slow-time concatenation of
@@ -35,7 +36,7 @@ def _frames_with_gaps(F, frame0_from=0, need_empty=2):
     return cfg, p, wr, wd, cal, iq
 
 
-def _device_path(engine, cfg, iq, halo=None, halo_len=None, nlog=0):
+def _device_path(engine, cfg, iq, halo=None, halo_len=None, nlog=0, direct=False):
     import torch
     F, C = iq.shape[0], cfg.pn
     dev = "cuda"
@@ -66,12 +67,19 @@ def _device_path(engine, cfg, iq, halo=None, halo_len=None, nlog=0):
         d_halo[: len(halo)] = torch.from_numpy(np.asarray(halo, np.float32))
         d_hl = torch.tensor([halo_len], dtype=torch.int64, device=dev)
         n_halo = h
-    engine.stft_power_device(outs["slow_mag"], flist, d_len, C, win, WLEN, NOV, NFFT, 1.0 / cfg.prt, max_seg,
-                             d_P, pmax, nseg, d_halo=d_halo, n_halo=n_halo, d_halo_len=d_hl, stream=s)
-    out = d_P
-    if nlog:
-        out = torch.empty((max_seg, nlog), dtype=torch.float32, device=dev)
-    engine.stft_db_device(d_P, nseg, max_seg, NFFT, 1.0 / cfg.prt, pmax, nlog, out, stream=s)
+    if direct:   # bench.py's form: pass 1 forms max(P) only, pass 2 recomputes P and writes dB (P never stored)
+        engine.stft_power_device(outs["slow_mag"], flist, d_len, C, win, WLEN, NOV, NFFT, 1.0 / cfg.prt, max_seg,
+                                 None, pmax, nseg, d_halo=d_halo, n_halo=n_halo, d_halo_len=d_hl, stream=s)
+        out = d_P
+        engine.stft_db_direct_device(outs["slow_mag"], flist, d_len, C, win, WLEN, NOV, NFFT, 1.0 / cfg.prt,
+                                     max_seg, pmax, out, d_halo=d_halo, n_halo=n_halo, d_halo_len=d_hl, stream=s)
+    else:
+        engine.stft_power_device(outs["slow_mag"], flist, d_len, C, win, WLEN, NOV, NFFT, 1.0 / cfg.prt, max_seg,
+                                 d_P, pmax, nseg, d_halo=d_halo, n_halo=n_halo, d_halo_len=d_hl, stream=s)
+        out = d_P
+        if nlog:
+            out = torch.empty((max_seg, nlog), dtype=torch.float32, device=dev)
+        engine.stft_db_device(d_P, nseg, max_seg, NFFT, 1.0 / cfg.prt, pmax, nlog, out, stream=s)
     torch.cuda.synchronize()
     ns = int(nseg.item())
     got = {k: v.cpu().numpy() for k, v in outs.items()}
@@ -90,10 +98,11 @@ def _check_db(got_psd, ref_psd):
     assert err <= TOL_FP32_DB, err
 
 
-def test_device_path_compact_stft_matches_oracle(engine):
+@pytest.mark.parametrize("direct", [False, True], ids=["stored_P", "direct_dB"])
+def test_device_path_compact_stft_matches_oracle(engine, direct):
     cfg, p, wr, wd, cal, iq = _frames_with_gaps(24, frame0_from=200)
     engine.set_taps(cfg, cal, wr, wd)
-    got = _device_path(engine, cfg, iq)
+    got = _device_path(engine, cfg, iq, direct=direct)
     ref = O.process_frames(iq, cal, p, wr, wd)
     # k_compact: the frames that feed the slow-time signal, in order, and L = PN * #frames (:257-260)
     keep = np.nonzero(ref["tgt_count"] > 0)[0]
@@ -117,15 +126,15 @@ def test_device_path_log_resampled(engine):
     _check_db(got["psd"], sr["intensity"])
 
 
-@pytest.mark.parametrize("halo_len", [19, 7, 0])
-def test_device_path_with_halo(engine, halo_len):
+@pytest.mark.parametrize("halo_len,direct", [(19, False), (7, False), (0, False), (19, True), (7, True)])
+def test_device_path_with_halo(engine, halo_len, direct):
     """Multi-GPU form: the shard's signal continues into the next shards' first
     samples (dist.right_halo); segments straddling the boundary use them."""
     cfg, p, wr, wd, cal, iq = _frames_with_gaps(12, frame0_from=4000, need_empty=1)
     engine.set_taps(cfg, cal, wr, wd)
     rng = np.random.default_rng(halo_len)
     halo = (np.abs(rng.standard_normal(WLEN - 1)) * 40).astype(np.float32)
-    got = _device_path(engine, cfg, iq, halo=halo, halo_len=halo_len)
+    got = _device_path(engine, cfg, iq, halo=halo, halo_len=halo_len, direct=direct)
     ref = O.process_frames(iq, cal, p, wr, wd)
     x = np.r_[O.slow_time_signal(ref), halo[:halo_len].astype(np.float64)]
     assert got["nseg"] == len(x) - NOV
