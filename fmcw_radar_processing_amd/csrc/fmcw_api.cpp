@@ -197,7 +197,7 @@ struct fmcw_ctx {
   PinBuf pin_in, pin_out;
   hipStream_t cin = nullptr, cout = nullptr;
   hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
-  DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out;
+  DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out, s_bins;
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
   DevBuf s_tab;                                // STFT 20-tap table W[nfft/2+1][20]
   int64_t chunk_frames = 0;
@@ -1104,6 +1104,35 @@ int fmcw_stft_png(fmcw_ctx* c, const float* x, int64_t L, const float* win, int3
                    width > 0 ? width : FMCW_PNG_DEFAULT_W, height > 0 ? height : FMCW_PNG_DEFAULT_H, png_bytes);
 }
 
+// A large device -> pageable-host copy on stream s, through the two pinned out slots of the
+// context: the DMA of piece i overlaps the host threads copying piece i-1 to the caller (and
+// taking its first-touch page faults in parallel). Returns once dst holds every byte.
+static int d2h_big(fmcw_ctx* c, void* dst, const void* d_src, size_t bytes, hipStream_t s) {
+  constexpr size_t kPiece = 32u << 20;
+  if (bytes < 2 * kPiece) {
+    HIPCHK(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return FMCW_OK;
+  }
+  CHK(c->pin_out.ensure(2 * kPiece));
+  const size_t n = (bytes + kPiece - 1) / kPiece;
+  auto piece = [&](size_t i) { return std::min(kPiece, bytes - i * kPiece); };
+  for (size_t i = 0; i <= n; ++i) {
+    if (i < n) {
+      const int b = (int)(i & 1);
+      HIPCHK(hipMemcpyAsync(c->pin_out.at(b * kPiece), static_cast<const char*>(d_src) + i * kPiece, piece(i),
+                            hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(c->ev_d2h[b], s));
+    }
+    if (i >= 1) {   // piece i-1 is in its pinned slot once its event fires; slot (i-1)&1 is reused by piece i+1
+      const int b = (int)((i - 1) & 1);
+      HIPCHK(hipEventSynchronize(c->ev_d2h[b]));
+      par_memcpy(static_cast<char*>(dst) + (i - 1) * kPiece, c->pin_out.at(b * kPiece), piece(i - 1));
+    }
+  }
+  return FMCW_OK;
+}
+
 static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap,
                      int32_t nfft, double fs, int32_t n_log_bins, float* T, float* freq, float* intensity,
                      const char* png_path, int32_t width, int32_t height, int64_t* png_bytes) {
@@ -1118,6 +1147,25 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
   const int nb = nf / 2 + 1;
   const int world = 1 + (int)c->peers.size();
   auto dev = [&](int g) { return g == 0 ? c : c->peers[g - 1]; };
+  const double df = fs / nf;
+  const int nq = png_path ? (int)std::min<int64_t>(nb - 1, (int64_t)std::floor(FMCW_PNG_FMAX_HZ / df) + 2) : 0;
+  // With the log-frequency output (:286-299) and the 20-tap window, P is formed only for the
+  // bins interp1 and the picture read: a max(P)-only pass over every bin, then those columns
+  // ([seg][ncolP], ascending bins). Otherwise every bin ([seg][nb]).
+  const bool sel_mode = n_log_bins > 0 && fmcw::stft_fast_path(wlen, hop);
+  std::vector<int32_t> bins, lidx;
+  std::vector<float> lw;
+  if (sel_mode) {
+    log_table(nf, fs, n_log_bins, lidx, lw, nullptr);
+    std::vector<int32_t> pos(nb, 0);
+    for (int32_t i0 : lidx) pos[i0] = pos[i0 + 1] = 1;
+    for (int k = 0; k < nq; ++k) pos[k] = 1;
+    if (png_path) pos[nb - 1] = 1;
+    for (int k = 0; k < nb; ++k)
+      if (pos[k]) { pos[k] = (int32_t)bins.size(); bins.push_back(k); }
+    for (auto& i0 : lidx) i0 = pos[i0];   // i0 and i0+1 are both listed, so they are adjacent columns
+  }
+  const int ncolP = sel_mode ? (int)bins.size() : nb;
   // Segments are sharded contiguously over the devices; device g takes the
   // samples its segments cover (its halo is simply the next samples of x).
   // 1) P and the local max(P) per device
@@ -1131,7 +1179,7 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     CHK(d->s_x.ensure((size_t)std::max<int64_t>(Ld, 1) * 4));
     CHK(d->s_list.ensure(4));
     CHK(d->s_len.ensure(8));
-    CHK(d->s_P.ensure((size_t)std::max<int64_t>(ns, 1) * nb * 4));
+    CHK(d->s_P.ensure((size_t)std::max<int64_t>(ns, 1) * ncolP * 4));
     CHK(d->s_pmax.ensure(4));
     CHK(d->s_nseg.ensure(8));
     CHK(d->s_win.ensure((size_t)wlen * 4));
@@ -1145,8 +1193,19 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     HIPCHK(hipMemcpyAsync(d->s_win.p, win, (size_t)wlen * 4, hipMemcpyHostToDevice, s));
     // the shard's samples are one "frame" of Ld samples in the compaction indirection
     CHK(fmcw_stft_power_device(d, d->s_x.as<float>(), d->s_list.as<int32_t>(), d->s_len.as<int64_t>(), (int32_t)Ld,
-                               nullptr, 0, nullptr, d->s_win.as<float>(), wlen, noverlap, nf, fs, ns, d->s_P.as<float>(),
-                               d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
+                               nullptr, 0, nullptr, d->s_win.as<float>(), wlen, noverlap, nf, fs, ns,
+                               sel_mode ? nullptr : d->s_P.as<float>(), d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
+    if (sel_mode) {   // second pass: P of the listed bins (the W table of the first pass is reused)
+      CHK(d->s_bins.ensure(bins.size() * 4));
+      HIPCHK(hipMemcpyAsync(d->s_bins.p, bins.data(), bins.size() * 4, hipMemcpyHostToDevice, s));
+      fmcw::StftArgs a{};
+      a.slow_mag = d->s_x.as<float>(); a.frame_list = d->s_list.as<int32_t>(); a.len = d->s_len.as<int64_t>();
+      a.pn = (int32_t)Ld; a.win = d->s_win.as<float>(); a.wlen = wlen; a.hop = hop; a.nfft = nf;
+      a.inv_fs = (float)(1.0 / fs); a.max_seg = ns; a.bins = d->s_bins.as<int32_t>(); a.ncol = ncolP;
+      StageTimer tm(d, 4, s);
+      HIPCHK(fmcw::launch_stft20(a, d->s_tab.as<float2>(), 3, d->s_P.as<float>(), s));
+      tm.done();
+    }
     HIPCHK(hipStreamSynchronize(s));   // the host-side scalars above go out of scope
   }
   // 2) the global max(P) of :282-283: RCCL all_reduce(max) across the devices
@@ -1177,8 +1236,6 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
   //     the bins below ylim plus the Nyquist bin of every segment, gathered to device 0
   std::vector<uint8_t> img;
   if (png_path) {
-    const double df = fs / nf;
-    const int nq = (int)std::min<int64_t>(nb - 1, (int64_t)std::floor(FMCW_PNG_FMAX_HZ / df) + 2);
     std::vector<float> q((size_t)std::max<int64_t>(nseg, 1) * (nq + 1));
     for (int g = 0; g < world; ++g) {
       fmcw_ctx* d = dev(g);
@@ -1186,10 +1243,11 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       shard(nseg, g, world, s0, ns);
       if (ns == 0) continue;
       CHK(set_device(d));
-      HIPCHK(hipMemcpy2DAsync(q.data() + s0 * (nq + 1), (nq + 1) * 4, d->s_P.p, (size_t)nb * 4, (size_t)nq * 4, ns,
+      // bins 0..nq-1 are the first nq columns of P and the Nyquist bin its last, in both layouts
+      HIPCHK(hipMemcpy2DAsync(q.data() + s0 * (nq + 1), (nq + 1) * 4, d->s_P.p, (size_t)ncolP * 4, (size_t)nq * 4, ns,
                               hipMemcpyDeviceToHost, d->stream));
-      HIPCHK(hipMemcpy2DAsync(q.data() + s0 * (nq + 1) + nq, (nq + 1) * 4, d->s_P.as<float>() + (nb - 1), (size_t)nb * 4,
-                              4, ns, hipMemcpyDeviceToHost, d->stream));
+      HIPCHK(hipMemcpy2DAsync(q.data() + s0 * (nq + 1) + nq, (nq + 1) * 4, d->s_P.as<float>() + (ncolP - 1),
+                              (size_t)ncolP * 4, 4, ns, hipMemcpyDeviceToHost, d->stream));
     }
     for (int g = 0; g < world; ++g) {
       CHK(set_device(dev(g)));
@@ -1216,10 +1274,24 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     if (ns == 0) continue;
     CHK(set_device(d));
     hipStream_t s = d->stream;
-    CHK(fmcw_stft_db_device(d, d->s_P.as<float>(), d->s_nseg.as<int64_t>(), ns, nf, fs, d->s_pmax.as<float>(),
-                            n_log_bins, n_log_bins > 0 ? d->s_out.as<float>() : d->s_P.as<float>(), s));
+    if (sel_mode) {   // interp1 over the listed columns (lidx holds column positions)
+      CHK(d->s_lidx.ensure(lidx.size() * 4));
+      CHK(d->s_lw.ensure(lw.size() * 4));
+      HIPCHK(hipMemcpyAsync(d->s_lidx.p, lidx.data(), lidx.size() * 4, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(d->s_lw.p, lw.data(), lw.size() * 4, hipMemcpyHostToDevice, s));
+      fmcw::StftDbArgs a{};
+      a.P = d->s_P.as<float>(); a.nseg = d->s_nseg.as<int64_t>(); a.max_seg = ns; a.nbins_in = ncolP;
+      a.pmax = d->s_pmax.as<float>(); a.nlog = n_log_bins;
+      a.lidx = d->s_lidx.as<int32_t>(); a.lw = d->s_lw.as<float>(); a.out = d->s_out.as<float>();
+      StageTimer tm(d, 5, s);
+      HIPCHK(fmcw::launch_stft_db(a, s));
+      tm.done();
+    } else {
+      CHK(fmcw_stft_db_device(d, d->s_P.as<float>(), d->s_nseg.as<int64_t>(), ns, nf, fs, d->s_pmax.as<float>(),
+                              n_log_bins, n_log_bins > 0 ? d->s_out.as<float>() : d->s_P.as<float>(), s));
+    }
     const float* res = n_log_bins > 0 ? d->s_out.as<float>() : d->s_P.as<float>();
-    HIPCHK(hipMemcpyAsync(intensity + s0 * nbo, res, (size_t)ns * nbo * 4, hipMemcpyDeviceToHost, s));
+    CHK(d2h_big(d, intensity + s0 * nbo, res, (size_t)ns * nbo * 4, s));
   }
   for (int g = 0; g < world; ++g) {
     CHK(set_device(dev(g)));

@@ -132,7 +132,12 @@ __global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
 // 64-bit division.  Output tiles of 256 segments x 32 bins go through LDS so the
 // stores are coalesced.  MODE 0: P (one-sided 'psd') + max(P); MODE 1: max(P)
 // only; MODE 2: psd = 20 log10(P / max) (:283) written directly (the P of a
-// second pass, recomputed instead of stored and re-read).
+// second pass, recomputed instead of stored and re-read); MODE 3: P of the
+// listed bins only (the host call's second pass: the bins the log-frequency
+// interp1 of :299 and the picture read, not all nfft/2+1).
+// blockIdx.y splits the columns into chunks of col_chunk (a multiple of 32), so a
+// call with few segments and a large nfft (the reference's nextpow2 rule on a
+// long signal) still fills the chip.
 // ---------------------------------------------------------------------------
 constexpr int STFT_W = 20;
 
@@ -148,7 +153,8 @@ __global__ __launch_bounds__(256) void k_stft_table(const float* __restrict__ wi
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __restrict__ tab, float* __restrict__ dst) {
+__global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __restrict__ tab, float* __restrict__ dst,
+                                                int col_chunk) {
   constexpr int TS = 256, KC = 32;
   __shared__ float xs[TS * 4 + STFT_W];         // hop <= 4 (the reference's is 1): 38 KiB of LDS, 4 blocks per CU
   __shared__ float tile[TS][KC + 1];
@@ -159,7 +165,7 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
   const int noverlap = STFT_W - a.hop;
   int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
   if (nseg > a.max_seg) nseg = a.max_seg;
-  if (MODE != 2 && blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+  if (MODE < 2 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
   const int64_t s0 = (int64_t)blockIdx.x * TS;
   if (s0 >= nseg) return;                                           // block-uniform
   const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
@@ -187,12 +193,16 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
     inv = pm > 0.f ? 1.0f / pm : 0.f;                               // all-zero P: -Inf dB (MATLAB G = 0)
   }
   const int nb = a.nfft / 2 + 1;
+  const int ncol = MODE == 3 ? a.ncol : nb;                         // output row length
+  const int c_lo = blockIdx.y * col_chunk;
+  const int c_hi = ncol - c_lo < col_chunk ? ncol : c_lo + col_chunk;
+  const __attribute__((address_space(4))) int* B = (const __attribute__((address_space(4))) int*)(const void*)a.bins;
   float lmax = 0.f;
-  for (int k0 = 0; k0 < nb; k0 += KC) {                             // uniform: bins k0 .. k0+KC-1
-    const int kn = nb - k0 < KC ? nb - k0 : KC;
+  for (int k0 = c_lo; k0 < c_hi; k0 += KC) {                        // uniform: columns k0 .. k0+KC-1
+    const int kn = c_hi - k0 < KC ? c_hi - k0 : KC;
 #pragma unroll 4
     for (int kk = 0; kk < kn; ++kk) {             // unrolled: the scalar table loads of 4 bins issue together
-      const int k = k0 + kk;
+      const int k = MODE == 3 ? B[k0 + kk] : k0 + kk;
       const auto* Wk = T + (int64_t)k * STFT_W;
       float re = 0.f, im = 0.f;
 #pragma unroll
@@ -204,20 +214,20 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
       const float g = (k == 0 || 2 * k == a.nfft) ? 1.f : 2.f;     // one-sided 'psd'
       const float p = fmaf(re, re, im * im) * scale * g;
       if (valid) lmax = fmaxf(lmax, p);
-      if constexpr (MODE == 0) tile[sl][kk] = p;
+      if constexpr (MODE == 0 || MODE == 3) tile[sl][kk] = p;
       if constexpr (MODE == 2) tile[sl][kk] = 20.0f * log10f(p * inv);
     }
     if constexpr (MODE != 1) {
       __syncthreads();
       float* out = MODE == 0 ? a.P : dst;
-      for (int i = threadIdx.x; i < ns * kn; i += 256) {            // row-major [seg][bin] chunk, coalesced per row
+      for (int i = threadIdx.x; i < ns * kn; i += 256) {            // row-major [seg][col] chunk, coalesced per row
         const int r = i / kn, c = i - r * kn;
-        out[(s0 + r) * nb + k0 + c] = tile[r][c];
+        out[(s0 + r) * ncol + k0 + c] = tile[r][c];
       }
       __syncthreads();
     }
   }
-  if constexpr (MODE != 2) {
+  if constexpr (MODE < 2) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
     if ((threadIdx.x & 63) == 0) bmax[threadIdx.x >> 6] = lmax;
@@ -342,11 +352,21 @@ hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_
 hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s) {
   if (a.max_seg <= 0) return hipSuccess;
   if (!stft_fast_path(a.wlen, a.hop)) return hipErrorInvalidValue;
+  if (mode == 3 && (!a.bins || a.ncol < 1)) return hipErrorInvalidValue;
   const int64_t blocks = (a.max_seg + 255) / 256;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
-  else if (mode == 1) hipLaunchKernelGGL(k_stft20<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
-  else hipLaunchKernelGGL(k_stft20<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+  // columns per y-block: enough y-blocks for ~2048 workgroups in all, in chunks of 32 columns
+  const int ncol = mode == 3 ? a.ncol : a.nfft / 2 + 1;
+  const int64_t chunks = (ncol + 31) / 32;
+  int64_t ysplit = (2048 + blocks - 1) / blocks;
+  if (ysplit > chunks) ysplit = chunks;
+  if (ysplit < 1) ysplit = 1;
+  const int col_chunk = (int)((chunks + ysplit - 1) / ysplit) * 32;
+  const dim3 grid((unsigned)blocks, (unsigned)((ncol + col_chunk - 1) / col_chunk));
+  if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+  else if (mode == 1) hipLaunchKernelGGL(k_stft20<1>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+  else if (mode == 2) hipLaunchKernelGGL(k_stft20<2>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+  else hipLaunchKernelGGL(k_stft20<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
   return hipGetLastError();
 }
 

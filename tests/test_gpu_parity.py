@@ -128,7 +128,7 @@ def test_deterministic(engine):
         np.testing.assert_array_equal(a[k], b[k])
 
 
-@pytest.mark.parametrize("L,nfft,nlog", [(19 * 16 + 1, 0, 1024), (16 * 115, 0, 1024), (2000, 64, 0), (500, 0, 0)])
+@pytest.mark.parametrize("L,nfft,nlog", [(19 * 16 + 1, 0, 1024), (16 * 115, 0, 1024), (5000, 0, 1024), (2000, 64, 0), (500, 0, 0)])
 def test_stft_matches_oracle(engine, L, nfft, nlog):
     rng = np.random.default_rng(L)
     x = np.abs(rng.standard_normal(L) + 3 * np.sin(np.arange(L) * 0.3)).astype(np.float32).astype(np.float64)
