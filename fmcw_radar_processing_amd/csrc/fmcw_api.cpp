@@ -698,17 +698,22 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     {   // diagnostic build: per-phase durations and concurrency of k_rd1p (100 MHz realtime clock)
       // stamps: 0 entry, 1 prologue issued, 2 wave 0 range loop done, 3 reductions done,
       //         4 Doppler stores issued, 5 stores drained
-      std::vector<unsigned long long> h(nblk * 8);
+#ifdef OP_STAMPS2
+      constexpr int NST = 16;
+#else
+      constexpr int NST = 8;
+#endif
+      std::vector<unsigned long long> h(nblk * NST);
       HIPCHK(hipStreamSynchronize(s));
       HIPCHK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
       unsigned long long lo = ~0ull, hi = 0;
       double ph[5] = {0, 0, 0, 0, 0};
       for (size_t i = 0; i < nblk; ++i) {
-        lo = std::min(lo, h[8 * i]); hi = std::max(hi, h[8 * i + 5]);
-        for (int q = 0; q < 5; ++q) ph[q] += (double)(h[8 * i + q + 1] - h[8 * i + q]);
+        lo = std::min(lo, h[NST * i]); hi = std::max(hi, h[NST * i + 5]);
+        for (int q = 0; q < 5; ++q) ph[q] += (double)(h[NST * i + q + 1] - h[NST * i + q]);
       }
       double w4 = 0, w7 = 0;   // range loop end of waves 4 and 7 (stamps 6, 7) after the prologue
-      for (size_t i = 0; i < nblk; ++i) { w4 += (double)(h[8 * i + 6] - h[8 * i + 1]); w7 += (double)(h[8 * i + 7] - h[8 * i + 1]); }
+      for (size_t i = 0; i < nblk; ++i) { w4 += (double)(h[NST * i + 6] - h[NST * i + 1]); w7 += (double)(h[NST * i + 7] - h[NST * i + 1]); }
       std::fprintf(stderr, "stamps-waves: range loop end after prologue (us): wave0 %.2f wave4 %.2f wave7 %.2f\n",
                    ph[1] / nblk / 100.0, w4 / nblk / 100.0, w7 / nblk / 100.0);
       const double span = (double)(hi - lo);
@@ -718,6 +723,20 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
                    "doppler %.2f drain %.2f (life %.2f) | avg resident %.1f\n", nblk, span / 100.0,
                    ph[0] / nblk / 100.0, ph[1] / nblk / 100.0, ph[2] / nblk / 100.0, ph[3] / nblk / 100.0,
                    ph[4] / nblk / 100.0, life / nblk / 100.0, life / span);
+#ifdef OP_STAMPS2
+      {   // wave 0's timeline from the range loop end: 2 -> B2 8 -> 3 -> 9 -> 10 -> B3 11 -> 12 -> 13 -> B4/B5 14 -> 4 -> 5
+        const int ord[] = {2, 8, 3, 9, 10, 11, 12, 13, 14, 4, 5};
+        const char* nm[] = {"B1+tile1+partials+B2", "reduce", "candidates", "pre0+stage0", "B3", "post0", "pre1",
+                            "B4+stage1+B5", "post1", "drain"};
+        std::string o;
+        for (int q = 0; q < 10; ++q) {
+          double d = 0;
+          for (size_t i = 0; i < nblk; ++i) d += (double)(h[NST * i + ord[q + 1]] - h[NST * i + ord[q]]);
+          o += std::string(nm[q]) + " " + std::to_string(d / nblk / 100.0).substr(0, 5) + " | ";
+        }
+        std::fprintf(stderr, "stamps-doppler (us): %s\n", o.c_str());
+      }
+#endif
     }
 #endif
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));

@@ -384,8 +384,16 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   const int t = (b >> 3) & 7;
   if (f >= a.F) return;                          // block-uniform
   const int S = FULL ? NR : a.S;
+#ifdef OP_STAMPS2
+#ifndef OP_STAMPS
+#define OP_STAMPS 1
+#endif
+#define OP_NST 16
+#else
+#define OP_NST 8
+#endif
 #ifdef OP_STAMPS
-  if (tid == 0) a.dbg[(int64_t)b * 8] = __builtin_amdgcn_s_memrealtime();
+  if (tid == 0) a.dbg[(int64_t)b * OP_NST] = __builtin_amdgcn_s_memrealtime();
 #endif
 #ifndef OP_ROT
 #define OP_ROT 1
@@ -420,8 +428,13 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   const int m0 = lane_bin(lane);
   const c2 w128 = tab[OP_TAB_LANE + 5 * 64 + lane];
   const int r0 = t + 8 * m0, r1 = r0 + 512;      // this lane's two range bins
+#ifdef OP_STAMPS2
+  auto stamp2 = [&](int i) { if (tid == 0) a.dbg[(int64_t)b * OP_NST + i] = __builtin_amdgcn_s_memrealtime(); };
+#else
+  auto stamp2 = [](int) {};
+#endif
 #ifdef OP_STAMPS
-  auto stamp = [&](int i) { if (tid == 0) a.dbg[(int64_t)b * 8 + i] = __builtin_amdgcn_s_memrealtime(); };
+  auto stamp = [&](int i) { if (tid == 0) a.dbg[(int64_t)b * OP_NST + i] = __builtin_amdgcn_s_memrealtime(); };
 #else
   auto stamp = [](int) {};
 #endif
@@ -549,7 +562,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
 #endif
   // ---------------- per-row reductions over the 8 waves --------------------
 #ifdef OP_STAMPS
-  if (lane == 0 && (w == 4 || w == 7)) a.dbg[(int64_t)b * 8 + (w == 4 ? 6 : 7)] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0 && (w == 4 || w == 7)) a.dbg[(int64_t)b * OP_NST + (w == 4 ? 6 : 7)] = __builtin_amdgcn_s_memrealtime();
 #endif
   stamp(2);
   __syncthreads();                               // B1: slot 1 complete in LDS
@@ -570,6 +583,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     L.red[1][w][0][lane] = s1.x; L.red[1][w][1][lane] = s1.y; L.red[1][w][2][lane] = p1;
   }
   __syncthreads();                               // B2: partials visible; L.t1 read out (free for the corner turn)
+  stamp2(8);
   // every wave reduces the 8 partials of its lane's two rows in the same order
   // (identical bits in every wave), so no serial section follows
   c2 mu0 = c2{0.f, 0.f}, mu1 = c2{0.f, 0.f};
@@ -628,6 +642,7 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
     }
   }
 
+  stamp2(9);
   // ---------------- Doppler: :217-219 on every row of the tile -------------
   // k = w + 8 k2, d = d2 + 32 d1: each lane's 32-point DFT over its own chirps
   // (W32^(k2 d2)), corner turn through LDS, twiddle W256^(w d2) by the reader,
@@ -734,16 +749,21 @@ __global__ __launch_bounds__(64 * op::NW, 1) void k_rd1p(OnePassArgs a) {
   };
   pre(tile0, mu0);
   stage(tile0);                                  // L.t1 was read out before B2; tile0 dies here
+  stamp2(10);
   __syncthreads();                               // B3: slot-0 corner turn written (and the candidate rows)
+  stamp2(11);
 #pragma unroll
   for (int c = 0; c < OP_CAND; ++c)
     if (csel[c] >= 0 && tid < C)
       a.cand_rows[((f * OP_TILES + t) * OP_CAND + c) * (int64_t)C + tid] = L.cand[c][(tid % NW) * CPW + ((tid / NW - rs) & (CPW - 1))];
   post(0);                                       // its LDS reads and stores overlap slot 1's DFT arithmetic
+  stamp2(12);
   pre(tile1, mu1);
+  stamp2(13);
   __syncthreads();                               // B4: slot-0 corner turn read out
   stage(tile1);
   __syncthreads();                               // B5
+  stamp2(14);
   post(1);
   stamp(4);
 #ifdef OP_STAMPS
