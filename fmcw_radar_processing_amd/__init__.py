@@ -4,7 +4,7 @@ Product code only: the HIP kernels live in libfmcw.so (csrc/), reached via the
 C-ABI of include/fmcw.h.  The test oracle lives in /oracle and is never
 imported from here.
 """
-from ._lib import (FMCW_C32H, FMCW_C64, FMCW_PIPE_AUTO, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS,  # noqa: F401
+from ._lib import (FMCW_C32H, FMCW_C64, FMCW_PIPE_AUTO, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS, FMCW_PIPE_XCD,  # noqa: F401
                    FmcwError)
 from .params import FmcwConfig, calibration, config, derive_params, deployed_device  # noqa: F401
 

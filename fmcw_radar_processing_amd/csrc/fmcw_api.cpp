@@ -204,6 +204,9 @@ struct fmcw_ctx {
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
   DevBuf op_gh, op_tab;                        // single-pass tables (fmcw::OP_TAB_*)
+  DevBuf x_cube, x_ctr, x_err, x_tab;          // XCD-team schedule: hand-off slots, counters, sticky error, XT_* table
+  int xcd_ok = -1;                             // census of the device (-1 not run yet)
+  bool xcd_used = false;                       // a k_rdx launch since the last error check
   float op_gh_scale = 0.f;                     // IF_scale op_gh was built for (0 = stale)
   // Multi-device context (fmcw_ctx_create with n_devices > 1): this object is
   // device 0 of the context and peers[i] a full context on device i + 1.  The
@@ -501,18 +504,31 @@ int fmcw_set_chunk_frames(fmcw_ctx* c, int64_t frames) {
 
 int fmcw_set_pipeline(fmcw_ctx* c, int32_t mode) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
-  if (mode != FMCW_PIPE_AUTO && mode != FMCW_PIPE_STREAMS && mode != FMCW_PIPE_ONEPASS)
+  if (mode != FMCW_PIPE_AUTO && mode != FMCW_PIPE_STREAMS && mode != FMCW_PIPE_ONEPASS && mode != FMCW_PIPE_XCD)
     return fail(FMCW_E_ARG, "bad pipeline mode");
   c->pipe_mode = mode;
   for (fmcw_ctx* q : c->peers) q->pipe_mode = mode;
   return FMCW_OK;
 }
 
+// The XCD-team schedule's sticky error word (kernels_xcd.hip): read after the
+// stream is idle; a set bit means the outputs of some k_rdx launch are invalid.
+static int xcd_check(fmcw_ctx* c) {
+  if (!c->xcd_used) return FMCW_OK;
+  unsigned e = 0;
+  HIPCHK(hipMemcpy(&e, c->x_err.p, sizeof(e), hipMemcpyDeviceToHost));
+  c->xcd_used = false;
+  if (!e) return FMCW_OK;
+  HIPCHK(hipMemset(c->x_err.p, 0, sizeof(e)));
+  return fail(FMCW_E_HIP, (e & 2) ? "XCD schedule: an XCD received more than 32 workgroups (outputs invalid)"
+                                  : "XCD schedule: a range-cube hand-off timed out (outputs invalid)");
+}
+
 int fmcw_synchronize(fmcw_ctx* c) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   CHK(set_device(c));
   HIPCHK(hipStreamSynchronize(c->stream));
-  return FMCW_OK;
+  return xcd_check(c);
 }
 
 int fmcw_timing_enable(fmcw_ctx* c, int32_t enable) {
@@ -625,6 +641,18 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
           put(fmcw::OP_TAB_CST + ((tt * 8 + j) * 2 + e) * 64 + l, (double)(float)cr[idx] * wv,
               (double)(float)ci[idx] * wv);
         }
+  {   // XCD-team schedule twiddles (kernels_xcd.hip), lane order [..][64]
+    std::vector<float> xt(2 * (size_t)fmcw::XT_SIZE);
+    auto xput = [&](int idx, int e1024) { xt[2 * idx] = (float)cr[e1024 & (NR - 1)]; xt[2 * idx + 1] = (float)ci[e1024 & (NR - 1)]; };
+    for (int l = 0; l < 64; ++l) {
+      for (int k1 = 1; k1 < 8; ++k1)
+        for (int e = 0; e < 2; ++e) xput(fmcw::XT_R1 + (2 * (k1 - 1) + e) * 64 + l, (2 * l + e) * k1);   // W1024^(a k1)
+      for (int s1 = 1; s1 < 16; ++s1) xput(fmcw::XT_R2 + (s1 - 1) * 64 + l, 8 * ((l & 7) * s1));      // W128^(a0 s1)
+      for (int d0 = 1; d0 < 16; ++d0) xput(fmcw::XT_D1 + (d0 - 1) * 64 + l, 4 * ((l & 15) * d0));     // W256^(q d0)
+    }
+    CHK(c->x_tab.ensure(xt.size() * 4));
+    HIPCHK(hipMemcpyAsync(c->x_tab.p, xt.data(), xt.size() * 4, hipMemcpyHostToDevice, s));
+  }
   CHK(c->op_gh.ensure(g.size() * 4));
   HIPCHK(hipMemcpyAsync(c->op_gh.p, g.data(), g.size() * 4, hipMemcpyHostToDevice, s));
   CHK(c->op_tab.ensure(tab.size() * 4));
@@ -639,12 +667,29 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
 // range cube; k_detect_1p runs the detection; k_slow_fix recomputes the rare
 // slow-time row that was not among a tile's candidates.  Chunks bound the
 // candidate scratch (OP_TILES*OP_CAND rows of PN floats per frame).
+// Hand-off slots per XCD of the XCD-team schedule (FMCW_XCD_SLOTS: 2 .. 4).
+static int xcd_slots() {
+  const char* e = std::getenv("FMCW_XCD_SLOTS");
+  const int v = e ? std::atoi(e) : 3;
+  return std::min(std::max(v, 2), fmcw::XCD_MAX_SLOTS);
+}
+
 static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int h, int64_t F, float* d_prof,
                            int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
-                           void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
+                           void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s, bool xcd) {
   const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
   const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : 8192);
-  constexpr int TC = fmcw::OP_TILES * fmcw::OP_CAND;
+  const int tiles = xcd ? fmcw::XCD_TILES : fmcw::OP_TILES, ncand = xcd ? fmcw::XCD_CAND : fmcw::OP_CAND;
+  const int TC = tiles * ncand;
+  const int slots = xcd_slots();
+  if (xcd) {
+    CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8));
+    CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
+    if (!c->x_err.p) {
+      CHK(c->x_err.ensure(sizeof(unsigned)));
+      HIPCHK(hipMemsetAsync(c->x_err.p, 0, sizeof(unsigned), s));
+    }
+  }
   CHK(c->op_rowpk.ensure((size_t)chunk * NR * 8));
   CHK(c->op_cidx.ensure((size_t)chunk * TC * 4));
   CHK(c->op_crows.ensure((size_t)chunk * TC * C * 4));
@@ -679,6 +724,8 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.cand_idx = c->op_cidx.as<int32_t>();
     a.cand_rows = c->op_crows.as<float>();
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
+    a.xcube = c->x_cube.as<float2>(); a.xctr = c->x_ctr.as<unsigned>(); a.xerr = c->x_err.as<unsigned>();
+    a.slots = slots; a.xtab = c->x_tab.as<float2>(); a.cal_sum = c->cal_sum;
     {
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;
@@ -691,7 +738,12 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
 #endif
     {
       StageTimer tm(c, 8, s, 2);
-      HIPCHK(fmcw::launch_onepass(a, s));
+      if (xcd) {
+        HIPCHK(fmcw::launch_xcd(a, s));
+        c->xcd_used = true;
+      } else {
+        HIPCHK(fmcw::launch_onepass(a, s));
+      }
       tm.done();
     }
 #ifdef OP_STAMPS
@@ -742,6 +794,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
     fmcw::Detect1pArgs k{};
     k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.rd_h = h; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
+    k.tiles = tiles; k.ncand = ncand;
     k.nframes = (int)nf; k.NR = NR; k.C = C; k.M = M;
     k.det.ND = ND; k.det.C = C; k.det.M = M;
     k.det.range_thr = p->range_thr; k.det.doppler_thr = p->doppler_thr;
@@ -787,12 +840,24 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const bool onepass_ok = !d_cube && (!d_rd || out_dtype == in_dtype) && fmcw::onepass_supported(S, C, NR, ND);
   // AUTO = single pass wherever it applies: half the HBM bytes of the streams
   // schedule (no range cube) and faster on MI355X
-  if (c->pipe_mode == FMCW_PIPE_ONEPASS || (c->pipe_mode == FMCW_PIPE_AUTO && onepass_ok)) {
+  if (c->pipe_mode == FMCW_PIPE_ONEPASS || c->pipe_mode == FMCW_PIPE_XCD || (c->pipe_mode == FMCW_PIPE_AUTO && onepass_ok)) {
     if (!onepass_ok)
       return fail(FMCW_E_ARG, "single-pass schedule: needs nr 1024, pn == nd == 256, even nts <= nr, "
                               "the RD map in the IQ dtype and no range cube");
+    bool xcd = false;
+    if (c->pipe_mode == FMCW_PIPE_XCD || c->pipe_mode == FMCW_PIPE_AUTO) {
+      if (c->xcd_ok < 0) {
+        int ok = 0;
+        HIPCHK(fmcw::xcd_census(&ok));
+        const char* e = std::getenv("FMCW_NO_XCD");
+        c->xcd_ok = ok && !(e && e[0] == '1');
+      }
+      if (c->pipe_mode == FMCW_PIPE_XCD && !c->xcd_ok)
+        return fail(FMCW_E_ARG, "XCD schedule: needs a 256-CU device that deals a 256-block grid 32 per XCD");
+      xcd = c->xcd_ok == 1;
+    }
     return process_onepass(c, p, d_iq, in_dtype == FMCW_C32H ? 1 : 0, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd, probe_column,
-                           d_probe, s);
+                           d_probe, s, xcd);
   }
   const int64_t chunk = c->chunk_frames > 0 ? c->chunk_frames : default_chunk(p);
   const int cube_dt = d_cube ? out_dtype : FMCW_C64;
@@ -1457,7 +1522,7 @@ static int process_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, i
   if (probe) HIPCHK(hipMemcpyAsync(probe, c->h_probe.p, (size_t)NR * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipStreamSynchronize(c->cout));
-  return FMCW_OK;
+  return xcd_check(c);
 }
 
 static int range_fft_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, int32_t in_dtype, int64_t F,

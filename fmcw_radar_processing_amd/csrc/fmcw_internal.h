@@ -96,15 +96,46 @@ struct OnePassArgs {
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
   unsigned long long* dbg; // diagnostic builds only (-DOP_STAMPS): [blocks][8] s_memrealtime stamps
+  // XCD-team schedule (k_rdx) only:
+  float2* xcube;           // [8 XCDs][slots][XCD_TILES groups][C][32] range-cube hand-off slots
+  unsigned* xctr;          // [8 XCDs][2: ready, done][XCD_MAX_SLOTS][32] + [8][32] tickets: one 128-byte line
+                           // per counter, XCD_CTR_WORDS in all (zeroed per launch)
+  unsigned* xerr;          // sticky: bit 0 a hand-off wait timed out, bit 1 an XCD got more than 32 blocks
+  int slots;               // hand-off slots per XCD (2 .. XCD_MAX_SLOTS)
+  const float2* xtab;      // XT_* sections (host, float64, lane order)
+  float2 cal_sum;          // sum_{n < S} cal[n]
 };
+
+// XCD-team schedule (kernels_xcd.hip): the 32 CUs of an XCD share each of its
+// frames, split by chirps for the range FFT and by range-bin groups for the
+// Doppler FFT; the range cube moves between them through the XCD's L2.
+constexpr int XCD_TILES = 32;        // range-bin groups per frame (one per team member)
+constexpr int XCD_CAND = 2;          // slow-time candidate rows kept per group
+constexpr int XCD_MAX_SLOTS = 4;
+constexpr int XCD_GRID = 256;        // 8 XCDs x 32 CUs, one persistent workgroup per CU
+constexpr int XCD_TICKETS = 8 * 2 * 32 * XCD_MAX_SLOTS;   // xctr offset of the 8 per-XCD member tickets (128-byte lines)
+constexpr int XCD_CTR_WORDS = XCD_TICKETS + 8 * 32;
+// table sections (float2, [..][64 lanes])
+constexpr int XT_R1 = 0;             // [14]: W1024^((2l + e) k1), index 2 (k1 - 1) + e
+constexpr int XT_R2 = 14 * 64;       // [15]: W128^((l & 7) s1), s1 = 1..15
+constexpr int XT_D1 = 29 * 64;       // [15]: W256^((l & 15) d0), d0 = 1..15
+constexpr int XT_SIZE = 44 * 64;
+// group g, position p (0..31) <-> range bin: r = k1 + 16 h + 8 e + 128 s2 with
+// k1 = (p >> 3) + 4 (g & 1), h = p & 7, e = (g >> 1) & 1, s2 = g >> 2
+__host__ __device__ inline int xcd_bin(int g, int p) {
+  return (p >> 3) + 4 * (g & 1) + 8 * ((g >> 1) & 1) + 16 * (p & 7) + 128 * (g >> 2);
+}
+__host__ __device__ inline int xcd_group(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1) | ((r >> 7) << 2); }
+__host__ __device__ inline int xcd_pos(int r) { return ((r & 3) << 3) | ((r >> 4) & 7); }
 
 struct Detect1pArgs {
   const float* profile;    // [F][NR]
   const int2* rowpk;       // [F][NR] (used when rd is nullptr)
   const void* rd;          // [F][NR][ND] c64 (c32h when rd_h, holding D * det.rd_unscale^-1) or nullptr
   int ND, rd_h;
-  const int32_t* cand_idx; // [F][OP_TILES][OP_CAND]
-  const float* cand_rows;  // [F][OP_TILES][OP_CAND][C] |X|^2
+  const int32_t* cand_idx; // [F][tiles][ncand]
+  const float* cand_rows;  // [F][tiles][ncand][C] |X|^2
+  int tiles, ncand;        // OP_TILES (tile = bin mod 8) / OP_CAND, or XCD_TILES (tile = xcd_group) / XCD_CAND
   int nframes, NR, C, M;
   DetectParams det;
   int32_t* count;
@@ -131,6 +162,8 @@ struct SlowFixArgs {
 
 hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s);
 hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s);
+hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s);
+hipError_t xcd_census(int* ok);      // 1 when the device places block b of a 256-block grid on XCD b mod 8
 hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s);
 
 struct ProbeArgs {          // fft_data column (:410-411) for the single-pass schedule

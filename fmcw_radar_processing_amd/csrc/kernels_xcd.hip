@@ -1,0 +1,431 @@
+// kernels_xcd.hip -- the XCD-team schedule of range + Doppler (k_rdx) for gfx950.
+//
+// The single pass (kernels_onepass.hip) splits a frame into 8 range tiles that
+// each re-read the whole 2 MiB frame from L2: 16 MiB of L2->CU traffic per
+// frame, which caps it near the L2 read ceiling.  Here the 32 CUs of one XCD
+// share a frame the way the reference computes it (radar_processing.m:199-219):
+//
+//   range   (:203-205): member k transforms chirps 8k .. 8k+7, one per wave,
+//                       as a full 1024-point FFT, and writes its 1024 bins of
+//                       each chirp into the XCD's hand-off slot as 32 groups
+//                       of 32 bins;
+//   Doppler (:210, :216-219): member k reads group k (32 range bins x 256
+//                       chirps, 64 KiB) back, takes the row means / maxima,
+//                       windows, runs 32 Doppler FFTs and writes its RD rows.
+//
+// So each input byte is read once, and the cube (2 MiB per frame) makes one
+// trip through the XCD's L2 instead of eight re-reads of the frame.  One
+// persistent 512-thread workgroup per CU; the 32 blocks that land on XCD x
+// (HW_REG_XCC_ID; xcd_census checks the 32-per-XCD deal before the schedule is
+// enabled) form its team, members k = 0..31 by ticket, and take frames x + 8 j.  Step
+// j runs R(j) then D(j-1), so the slot of frame j-1 is complete (all 32
+// members published) before anyone reads it; a ring of `slots` slots per XCD
+// with ready / done counters keeps a member from overwriting a slot that is
+// still being read.
+//
+// Hand-off protocol (tools/xcd_probe.hip measured it at 0.99 M frames/s of
+// pure data movement): producers store the slot with plain stores (the lines
+// stay in the XCD's L2), `s_waitcnt vmcnt(0)` in every wave, a workgroup
+// barrier, then one agent-scope atomic add on the slot's ready counter.
+// Consumers poll with relaxed agent loads (global_load sc1), then read the
+// slot with sc1 loads, which bypass the CU's L1 and are served by the XCD's L2.
+// Producer and consumer are on the same XCD, so no L2 write-back is needed.
+// Every wait is bounded: a timeout sets xerr bit 0 and lets the grid drain.
+//
+// Range FFT of one chirp in one wave (n = a + 128 i, r = k1 + 8 (s1 + 16 s2),
+// a = a0 + 8 a1):  lane l holds samples n = 2l + e + 128 i (8 16-byte loads);
+//   stage 1: DFT8 over i of both a = 2l + e, twiddle W1024^(a k1);
+//   LDS transpose; stage 2: lane 8 k1 + a0 runs DFT16 over a1, twiddle W128^(a0 s1);
+//   LDS transpose; stage 3: lane 8 k1 + h runs DFT8 over a0 for s1 = 2h, 2h + 1;
+// giving bins r = k1 + 16 h + 8 e + 128 s2: for a fixed register (e, s2) the 32
+// lanes of each half-wave hold the 32 bins of one group (xcd_bin), so every
+// slot store is a contiguous 256-byte row.
+// Doppler of one group: 64 KiB staged through LDS, lane (pp, q) of wave w holds
+// bin p = 4w + pp at chirps q + 16 i; DFT16 over i, twiddle W256^(q d0), LDS
+// transpose, DFT16 over q: D[d0 + 16 d1] in lane (pp, d0); fftshift is the
+// store index.
+#include "op_math.h"
+
+#include <cstdio>
+#include <cstdlib>
+
+namespace fmcw {
+namespace xk {
+using namespace op;
+
+constexpr int NK = 32;                 // team members (CUs) per XCD
+constexpr int C = 256;                 // chirps = Doppler points
+constexpr int NW = 8;                  // waves per workgroup = chirps per member
+constexpr int GP = 32;                 // bins per group
+static_assert(NK * NW == C && NK * GP == NR && NK == XCD_TILES, "team geometry");
+
+struct LdsX {
+  union {
+    f4v stg[C * 17];                   // Doppler staging [chirp][34 c2]: 32 bins + 2 pad (conflict-free both ways)
+    c2 rt[NW][1216];                   // per-wave transposes: range 8 x 136 and 64 x 18, Doppler 4 x 304
+  } u;
+  c2 twr1[14][64];
+  c2 twr2[15][64];
+  c2 twd1[15][64];
+  float wdl[16][64];                   // 2chebwin of chirp (l & 15) + 16 i
+  float key[GP];                       // candidate key per group position (profile or -1)
+};
+
+__device__ __forceinline__ unsigned ld_flag(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Bounded wait for *p >= v (one lane).  ~1 s before giving up; once any wait of
+// the launch timed out, the others return at once so the grid drains.
+__device__ __noinline__ void wait_ge(unsigned* p, unsigned v, unsigned* err) {
+  for (int it = 0; it < (1 << 20); ++it) {
+    if (ld_flag(p) >= v) return;
+    if ((it & 63) == 63 && ld_flag(err)) return;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  atomicOr(err, 1u);
+}
+__device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
+
+// row (16-lane group) reductions by DPP: symmetric pairings, every lane of the row gets the result
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  return v + dppf<0x140>(v);
+}
+__device__ __forceinline__ int row_max16(int v) {
+  v = max(v, dppi<0xB1>(v));
+  v = max(v, dppi<0x4E>(v));
+  v = max(v, dppi<0x141>(v));
+  return max(v, dppi<0x140>(v));
+}
+__device__ __forceinline__ int row_min16(int v) {
+  v = min(v, dppi<0xB1>(v));
+  v = min(v, dppi<0x4E>(v));
+  v = min(v, dppi<0x141>(v));
+  return min(v, dppi<0x140>(v));
+}
+
+}  // namespace xk
+
+template <bool FULL, bool H>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
+__global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
+  using namespace xk;
+  __shared__ __attribute__((aligned(16))) LdsX L;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // Team = the workgroups on one XCD (they share its L2).  The dispatcher deals
+  // blocks round-robin over the 8 XCDs from wherever the previous launch
+  // stopped, so the XCD is read from HW_REG_XCC_ID and the member index is a
+  // ticket drawn on that XCD's counter: 256 blocks give every XCD exactly 32.
+  __shared__ int team[2];
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const int xx = (int)(xcc & 7);
+    const int kk = (int)__hip_atomic_fetch_add(a.xctr + XCD_TICKETS + xx * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kk >= NK) atomicOr(a.xerr, 2u);
+    team[0] = xx;
+    team[1] = kk;
+  }
+  __syncthreads();
+  const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
+  if (k >= NK) return;                 // more than 32 blocks on one XCD: its team is short (waits time out)
+  const int nj = a.F > x ? (int)((a.F - x + 7) / 8) : 0;   // frames x + 8 j of this XCD
+  const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
+  unsigned* ready = a.xctr + (x * 2 + 0) * 32 * XCD_MAX_SLOTS;
+  unsigned* done = a.xctr + (x * 2 + 1) * 32 * XCD_MAX_SLOTS;
+
+  for (int i = tid; i < 44 * 64; i += 512) {
+    const c2 v = tov(a.xtab[i]);
+    if (i < XT_R2) L.twr1[i >> 6][i & 63] = v;
+    else if (i < XT_D1) L.twr2[(i - XT_R2) >> 6][i & 63] = v;
+    else L.twd1[(i - XT_D1) >> 6][i & 63] = v;
+  }
+  for (int i = tid; i < 16 * 64; i += 512) L.wdl[i >> 6][i & 63] = a.wd[(i & 15) + 16 * (i >> 6)];
+  // :203-205 per-lane constants of samples n = 2 lane + e + 128 i: w' = IF_scale 2blackman, cal w'
+  float wp[16];
+  c2 cw[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int n = 2 * lane + e + 128 * i;
+      const float4 cv = n < S ? a.calw[n] : make_float4(0.f, 0.f, 0.f, 0.f);
+      wp[2 * i + e] = cv.z;
+      cw[2 * i + e] = c2{cv.x * cv.z, cv.y * cv.z};
+    }
+  const c2 csum = c2{a.cal_sum.x, a.cal_sum.y};
+  const float invS = 1.0f / (float)S;
+  __syncthreads();
+
+  using TP = std::conditional_t<H, h4v, f4v>;
+  const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
+  auto ld_chirp = [&](int64_t f, TP (&xin)[8]) {
+    const TP* __restrict__ q = iq + (f * C + (k * NW + w)) * (int64_t)S2;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int p = lane + 64 * i;
+      if constexpr (FULL) xin[i] = __builtin_nontemporal_load(q + p);
+      else xin[i] = __builtin_nontemporal_load(q + (p < S2 ? p : 0));
+    }
+  };
+
+  // ---------------- R: one chirp per wave (:203-205) ----------------
+  auto range = [&](const TP (&xin)[8], c2* __restrict__ slot) {
+    c2 v[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f4v t;
+      if constexpr (H) t = __builtin_convertvector(xin[i], f4v);
+      else t = xin[i];
+      if constexpr (!FULL)
+        if (!(lane + 64 * i < S2)) t = f4v{0.f, 0.f, 0.f, 0.f};
+      v[2 * i] = t.xy;
+      v[2 * i + 1] = t.zw;
+    }
+    c2 sm = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+    for (int n = 4; n < 16; n += 4) sm += (v[n] + v[n + 1]) + (v[n + 2] + v[n + 3]);
+    const c2 mu = (wave_sum_c(sm) - csum) * invS;       // :204 mean of (x - cal) over the chirp
+#pragma unroll
+    for (int n = 0; n < 16; ++n) v[n] = __builtin_elementwise_fma(v[n] - mu, c2{wp[n], wp[n]}, -cw[n]);   // (x - cal - mu) w'
+    c2 z0[8], z1[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { z0[i] = v[2 * i]; z1[i] = v[2 * i + 1]; }
+    dft8p(z0);
+    dft8p(z1);
+#pragma unroll
+    for (int k1 = 1; k1 < 8; ++k1) {
+      z0[k1] = cmul_a(z0[k1], L.twr1[2 * (k1 - 1)][lane]);
+      z1[k1] = cmul_a(z1[k1], L.twr1[2 * (k1 - 1) + 1][lane]);
+    }
+    c2* rt = L.u.rt[w];
+#pragma unroll
+    for (int k1 = 0; k1 < 8; ++k1)
+      *reinterpret_cast<f4v*>(&rt[k1 * 136 + 2 * lane]) = f4v{z0[k1].x, z0[k1].y, z1[k1].x, z1[k1].y};
+    cfence();
+    const int k1 = lane >> 3, a0 = lane & 7;
+    c2 u[16];
+#pragma unroll
+    for (int a1 = 0; a1 < 16; ++a1) u[a1] = rt[k1 * 136 + a0 + 8 * a1];
+    cfence();
+    dft16p<1>(u);
+#pragma unroll
+    for (int s1 = 1; s1 < 16; ++s1) u[s1] = cmul_a(u[s1], L.twr2[s1 - 1][lane]);
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+      *reinterpret_cast<f4v*>(&rt[lane * 18 + 2 * h]) = f4v{u[2 * h].x, u[2 * h].y, u[2 * h + 1].x, u[2 * h + 1].y};
+    cfence();
+    const int hh = lane & 7;
+    c2 q0[8], q1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const f4v t = *reinterpret_cast<const f4v*>(&rt[(k1 * 8 + j) * 18 + 2 * hh]);
+      q0[j] = t.xy;
+      q1[j] = t.zw;
+    }
+    cfence();
+    dft8p(q0);
+    dft8p(q1);
+    // bins k1 + 16 hh + 8 e + 128 s2 -> group 4 s2 + 2 e + (k1 >> 2), position lane & 31
+    const int c = k * NW + w;
+    c2* __restrict__ o = slot + (int64_t)((lane >> 5) * C + c) * GP + (lane & 31);
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) {
+      o[(int64_t)(4 * s2) * C * GP] = q0[s2];
+      o[(int64_t)(4 * s2 + 2) * C * GP] = q1[s2];
+    }
+  };
+
+  // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259) ----------------
+  auto doppler = [&](int64_t f, const c2* __restrict__ grp, unsigned* done_ctr) {
+    {
+      f4v t[8];
+      const f4v* __restrict__ gp = reinterpret_cast<const f4v*>(grp);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(t[i]) : "v"(gp + tid + 512 * i) : "memory");
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
+                   "+v"(t[6]), "+v"(t[7]) :: "memory");
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e4 = tid + 512 * i;
+        L.u.stg[(e4 >> 4) * 17 + (e4 & 15)] = t[i];
+      }
+    }
+    __syncthreads();                   // staged: every load of the slot has returned
+    if (tid == 0) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
+    const int r = xcd_bin(k, p);
+    c2 xv[16];
+    {
+      const c2* stg = reinterpret_cast<const c2*>(L.u.stg);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) xv[i] = stg[(q + 16 * i) * 34 + p];
+    }
+    __syncthreads();                   // staging read out (the transposes reuse it)
+    // :217 row mean and :210 / :265 row max |X| over the 256 chirps
+    c2 sm = (xv[0] + xv[1]) + (xv[2] + xv[3]);
+    float pm = fmaxf(fmaxf(abs2v(xv[0]), abs2v(xv[1])), fmaxf(abs2v(xv[2]), abs2v(xv[3])));
+#pragma unroll
+    for (int i = 4; i < 16; i += 4) {
+      sm += (xv[i] + xv[i + 1]) + (xv[i + 2] + xv[i + 3]);
+      pm = fmaxf(pm, fmaxf(fmaxf(abs2v(xv[i]), abs2v(xv[i + 1])), fmaxf(abs2v(xv[i + 2]), abs2v(xv[i + 3]))));
+    }
+    sm = c2{row_sum16(sm.x), row_sum16(sm.y)};
+    pm = __int_as_float(row_max16(__float_as_int(pm)));
+    const c2 mu = sm * (1.0f / (float)C);
+    const float pr = sqrtf(pm);
+    if (q == 0) {
+      a.profile[f * NR + r] = pr;
+      const double rng = (double)r * a.dist_per_bin;
+      L.key[p] = (r >= 1 && r <= NR - 2 && rng >= a.min_d && rng <= a.max_d && pr > a.range_thr) ? pr : -1.f;
+    }
+    __syncthreads();                   // keys of all 32 rows
+    {   // slow-time candidates (:257-259): the XCD_CAND strongest in-window rows of the group
+      float kv = lane < GP ? L.key[lane] : -1.f;
+      const int ki = xcd_bin(k, lane & (GP - 1));
+#pragma unroll
+      for (int c = 0; c < XCD_CAND; ++c) {
+        float bv = kv;
+        int bi = ki;
+        wave_argmax_dpp(bv, bi);                               // same in every wave: ties -> lowest bin
+        const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
+        if (w == 0 && lane == 0) a.cand_idx[(f * XCD_TILES + k) * XCD_CAND + c] = sel;
+        if (sel >= 0 && r == sel) {
+          float* __restrict__ row = a.cand_rows + ((f * XCD_TILES + k) * XCD_CAND + c) * (int64_t)C;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) row[q + 16 * i] = abs2v(xv[i]);
+        }
+        if (ki == sel) kv = -1.f;
+      }
+    }
+    // :218 (X - mean) .* 2chebwin, :219 fft over chirps
+#pragma unroll
+    for (int i = 0; i < 16; ++i) xv[i] = (xv[i] - mu) * L.wdl[i][lane];
+    dft16p<1>(xv);
+#pragma unroll
+    for (int d0 = 1; d0 < 16; ++d0) xv[d0] = cmul_a(xv[d0], L.twd1[d0 - 1][lane]);
+    c2* rt = L.u.rt[w];
+#pragma unroll
+    for (int h = 0; h < 8; ++h)
+      *reinterpret_cast<f4v*>(&rt[304 * pp + 18 * q + 2 * h]) = f4v{xv[2 * h].x, xv[2 * h].y, xv[2 * h + 1].x, xv[2 * h + 1].y};
+    cfence();
+#pragma unroll
+    for (int m0 = 0; m0 < 16; ++m0) xv[m0] = rt[304 * pp + 18 * m0 + q];
+    cfence();
+    dft16p<1>(xv);                     // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
+    // :219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)]
+    if (a.rd) {
+      if constexpr (H) {
+        __half2* __restrict__ out = reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + q;
+#pragma unroll
+        for (int d1s = 0; d1s < 16; ++d1s) {
+          const c2 o = xv[(d1s + 8) & 15] * a.rd_scale;
+          out[16 * d1s] = __floats2half2_rn(o.x, o.y);
+        }
+      } else {
+        f2v* __restrict__ out = reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + q;
+#pragma unroll
+        for (int d1s = 0; d1s < 16; ++d1s) __builtin_nontemporal_store(xv[(d1s + 8) & 15], out + 16 * d1s);
+      }
+    } else {   // :233 [val, di] = max(abs(.)) of the row: exact max of |D|^2, then its first position
+      float m = abs2v(xv[8]);
+#pragma unroll
+      for (int d1s = 1; d1s < 16; ++d1s) m = fmaxf(m, abs2v(xv[(d1s + 8) & 15]));
+      const float rm = __int_as_float(row_max16(__float_as_int(m)));
+      int e = INT_MAX;
+#pragma unroll
+      for (int d1s = 15; d1s >= 0; --d1s)
+        if (abs2v(xv[(d1s + 8) & 15]) == rm) e = q + 16 * d1s;
+      e = row_min16(e);
+      if (q == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
+    }
+  };
+
+  TP xin[8];
+  if (nj > 0) ld_chirp(x, xin);
+  for (int j = 0; j <= nj; ++j) {
+    if (j < nj) {
+      const int s = j % NS;
+      if (j >= NS) {                   // slot s free: all members read frame j - NS out of it
+        if (tid == 0) wait_ge(&done[s * 32], (unsigned)(NK * (j / NS)), a.xerr);
+        __syncthreads();
+      }
+      range(xin, reinterpret_cast<c2*>(a.xcube) + (int64_t)(x * NS + s) * (NK * C * GP));
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();                 // every wave's slot stores are in the L2
+      if (tid == 0) __hip_atomic_fetch_add(&ready[s * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j + 1 < nj) ld_chirp(x + 8 * (int64_t)(j + 1), xin);   // next chirp in flight during D(j - 1)
+    }
+    if (j >= 1) {
+      const int jj = j - 1, s = jj % NS;
+      if (tid == 0) wait_ge(&ready[s * 32], (unsigned)(NK * (jj / NS + 1)), a.xerr);
+      __syncthreads();
+      doppler(x + 8 * (int64_t)jj, reinterpret_cast<const c2*>(a.xcube) + (int64_t)(x * NS + s) * (NK * C * GP) + (int64_t)k * C * GP, &done[s * 32]);
+    }
+  }
+}
+
+// One 256-block grid shaped like k_rdx (512 threads, the same LDS): block b
+// records the XCD it runs on; k_rdx needs 32 blocks on each of the 8 XCDs.
+// (dynamic LDS of sizeof(LdsX): one workgroup per CU, as k_rdx)
+__global__ __launch_bounds__(512, 1) void k_xcd_census(int* out) {
+  if (threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    out[blockIdx.x] = (int)(xcc & 15);
+  }
+}
+
+hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
+  if (a.F <= 0) return hipSuccess;
+  if (!onepass_supported(a.S, a.C, op::NR, a.C) || a.slots < 2 || a.slots > XCD_MAX_SLOTS) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s);
+  if (e != hipSuccess) return e;
+  const dim3 g(XCD_GRID), bl(64 * xk::NW);
+  if (a.S == op::NR) {
+    if (a.h) hipLaunchKernelGGL((k_rdx<true, true>), g, bl, 0, s, a);
+    else hipLaunchKernelGGL((k_rdx<true, false>), g, bl, 0, s, a);
+  } else {
+    if (a.h) hipLaunchKernelGGL((k_rdx<false, true>), g, bl, 0, s, a);
+    else hipLaunchKernelGGL((k_rdx<false, false>), g, bl, 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t xcd_census(int* ok) {
+  *ok = 0;
+  int dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e != hipSuccess) return e;
+  if (cus != XCD_GRID) {                    // the team geometry needs 8 XCDs x 32 CUs
+    if (const char* v = std::getenv("FMCW_XCD_DEBUG"); v && v[0] == '1') std::fprintf(stderr, "xcd_census: %d CUs\n", cus);
+    return hipSuccess;
+  }
+  int* d = nullptr;
+  if ((e = hipMalloc(&d, XCD_GRID * sizeof(int))) != hipSuccess) return e;
+  int h[XCD_GRID];
+  hipLaunchKernelGGL(k_xcd_census, dim3(XCD_GRID), dim3(512), sizeof(xk::LdsX), 0, d);
+  e = hipGetLastError();
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return e;
+  int n[8] = {}, good = 1;
+  for (int b = 0; b < XCD_GRID; ++b) {
+    if (h[b] < 0 || h[b] > 7) good = 0;
+    else ++n[h[b]];
+  }
+  for (int i = 0; i < 8; ++i) good &= n[i] == XCD_GRID / 8;
+  *ok = good;
+  if (const char* v = std::getenv("FMCW_XCD_DEBUG"); v && v[0] == '1') {
+    std::fprintf(stderr, "xcd_census: cus %d ok %d, XCC of blocks 0..15:", cus, good);
+    for (int b = 0; b < 16; ++b) std::fprintf(stderr, " %d", h[b]);
+    std::fprintf(stderr, "\n");
+  }
+  return hipSuccess;
+}
+
+}  // namespace fmcw

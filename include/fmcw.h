@@ -241,7 +241,7 @@ int fmcw_timing_reset(fmcw_ctx* ctx);
 int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
 
 /* Schedule of fmcw_process_device / fmcw_process (the two agree to fp32 rounding):
- *  FMCW_PIPE_AUTO    the single pass where it applies (geometry below, no
+ *  FMCW_PIPE_AUTO    a single-pass schedule where it applies (geometry below, no
  *                    range cube requested), else the streams schedule;
  *  FMCW_PIPE_STREAMS K1 | K2 | K3 kernels as a 3-stream chunk pipeline, the
  *                    range cube of each chunk round-trips through HBM;
@@ -251,8 +251,19 @@ int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
  *                    range cube never reaches memory.  Needs nr 1024,
  *                    pn == nd == 256, even nts <= nr, the RD map (if any) in the
  *                    IQ dtype (complex64 or fp16 storage), no range cube (else E_ARG).
+ *  FMCW_PIPE_XCD     the XCD-team schedule (kernels_xcd.hip): the same geometry
+ *                    and outputs as FMCW_PIPE_ONEPASS, but the 32 CUs of each XCD
+ *                    share a frame (range FFT split by chirps, Doppler FFT by
+ *                    range-bin groups, the cube handed over in the XCD's L2), so
+ *                    every input byte is read once.  One persistent workgroup per
+ *                    CU: needs a 256-CU device that deals a 256-block grid 32
+ *                    per XCD (checked once per context, else E_ARG); a hand-off that does
+ *                    not complete within ~1 s is reported by fmcw_synchronize
+ *                    (and the host-pointer calls) as FMCW_E_HIP.
+ * AUTO picks FMCW_PIPE_XCD where it applies and the device passes the check,
+ * else FMCW_PIPE_ONEPASS where that applies.
  * (Value 2 is retired: the persistent "fused" schedule of ABI 1, slower than both.) */
-enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_ONEPASS = 3 };
+enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_ONEPASS = 3, FMCW_PIPE_XCD = 4 };
 int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode);
 
 int fmcw_synchronize(fmcw_ctx* ctx);

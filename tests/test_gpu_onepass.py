@@ -9,7 +9,7 @@ SURVEY.md 8d tolerances against the oracle.
 import numpy as np
 import pytest
 
-from fmcw_radar_processing_amd import FMCW_PIPE_AUTO, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS, FmcwError
+from fmcw_radar_processing_amd import FMCW_PIPE_AUTO, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS, FMCW_PIPE_XCD, FmcwError
 from fmcw_radar_processing_amd import params as P
 from oracle import oracle as O
 from tests.helpers import TOL_FP32_REL_L2, case, near_tie_frames, rd_rel_err, rel_l2
@@ -23,9 +23,10 @@ def _frames(F, nts=1024, frame0=0):
     return cfg, p, wr, wd, cal, iq
 
 
-@pytest.fixture
-def onepass(engine):
-    engine.set_pipeline(FMCW_PIPE_ONEPASS)
+# both single-pass schedules: 8 range tiles per frame (k_rd1p) and the XCD team (k_rdx)
+@pytest.fixture(params=[FMCW_PIPE_ONEPASS, FMCW_PIPE_XCD], ids=["tiles8", "xcd"])
+def onepass(engine, request):
+    engine.set_pipeline(request.param)
     yield engine
     engine.set_pipeline(FMCW_PIPE_AUTO)
     engine.set_chunk_frames(0)
@@ -193,4 +194,64 @@ def test_onepass_fp16_matches_streams_fp16(engine):
         engine.set_pipeline(FMCW_PIPE_AUTO)
     assert (rel_l2(a["rd"].reshape(F, -1), b["rd"].reshape(F, -1), axis=1) <= TOL_FP16_REL_L2).all()
     for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+# ---- the XCD-team schedule (kernels_xcd.hip) on its own ----------------------
+@pytest.mark.parametrize("slots", ["2", "3", "4"])
+def test_xcd_slot_ring(engine, monkeypatch, slots):
+    """Frames 8 per XCD step: 75 frames = 9-10 steps per team, so every slot of
+    the hand-off ring is reused several times; outputs equal the 8-tile single
+    pass to fp32 rounding and the oracle within the fp32 bars, for any ring depth."""
+    monkeypatch.setenv("FMCW_XCD_SLOTS", slots)
+    F = 75
+    cfg, p, wr, wd, cal, iq = _frames(F, frame0=5000)
+    engine.set_taps(cfg, cal, wr, wd)
+    try:
+        engine.set_pipeline(FMCW_PIPE_XCD)
+        a = engine.process(iq, want_rd=True, probe_column=F * 256)
+        engine.synchronize()                       # no hand-off error reported
+        engine.set_pipeline(FMCW_PIPE_ONEPASS)
+        b = engine.process(iq, want_rd=True, probe_column=F * 256)
+    finally:
+        engine.set_pipeline(FMCW_PIPE_AUTO)
+    ref = O.process_frames(iq, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
+    _check_vs_oracle(cfg, a, ref, wd, F * 256)
+    for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    assert rel_l2(a["rd"], b["rd"], axis=(1, 2)).max() <= 2 * TOL_FP32_REL_L2
+
+
+def test_xcd_deterministic_and_chunked(engine):
+    """Two runs are bit-identical, and so are chunks of 13 frames (partial teams)."""
+    F = 40
+    cfg, p, wr, wd, cal, iq = _frames(F, frame0=777)
+    engine.set_taps(cfg, cal, wr, wd)
+    try:
+        engine.set_pipeline(FMCW_PIPE_XCD)
+        a = engine.process(iq, want_rd=True)
+        b = engine.process(iq, want_rd=True)
+        engine.set_chunk_frames(13)
+        c = engine.process(iq, want_rd=True)
+    finally:
+        engine.set_chunk_frames(0)
+        engine.set_pipeline(FMCW_PIPE_AUTO)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+        np.testing.assert_array_equal(a[k], c[k], err_msg=k)
+
+
+def test_auto_picks_xcd(engine):
+    """AUTO selects the XCD schedule for config-3/4 geometry: bit-identical to FMCW_PIPE_XCD."""
+    F = 16
+    cfg, p, wr, wd, cal, iq = _frames(F, frame0=31)
+    engine.set_taps(cfg, cal, wr, wd)
+    try:
+        engine.set_pipeline(FMCW_PIPE_AUTO)
+        a = engine.process(iq, want_rd=True)
+        engine.set_pipeline(FMCW_PIPE_XCD)
+        b = engine.process(iq, want_rd=True)
+    finally:
+        engine.set_pipeline(FMCW_PIPE_AUTO)
+    for k in a:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)

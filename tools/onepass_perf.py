@@ -10,7 +10,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from fmcw_radar_processing_amd import FMCW_C64, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS  # noqa: E402
+from fmcw_radar_processing_amd import FMCW_C64, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS, FMCW_PIPE_XCD  # noqa: E402
 from fmcw_radar_processing_amd import params as P  # noqa: E402
 from fmcw_radar_processing_amd.engine import Engine  # noqa: E402
 
@@ -31,7 +31,7 @@ def main(F=4096, reps=10, which="streams,onepass"):
                 slow_mag=torch.empty((F, cfg.pn), device=dev))
     d_rd = torch.empty((F, cfg.nr, cfg.nd, 2), dtype=torch.float32, device=dev)
     byt = F * (cfg.pn * cfg.nts * 8 + cfg.nr * cfg.nd * 8 + cfg.nr * 4 + cfg.pn * 4)
-    modes = {"streams": FMCW_PIPE_STREAMS, "onepass": FMCW_PIPE_ONEPASS}
+    modes = {"streams": FMCW_PIPE_STREAMS, "onepass": FMCW_PIPE_ONEPASS, "xcd": FMCW_PIPE_XCD}
     for name in which.split(","):
         mode = modes[name]
         e.set_pipeline(mode)
