@@ -667,11 +667,11 @@ static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
 // range cube; k_detect_1p runs the detection; k_slow_fix recomputes the rare
 // slow-time row that was not among a tile's candidates.  Chunks bound the
 // candidate scratch (OP_TILES*OP_CAND rows of PN floats per frame).
-// Hand-off slots per XCD of the XCD-team schedule (FMCW_XCD_SLOTS: 2 .. 4).
+// Hand-off slots per XCD of the XCD-team schedule (4; FMCW_XCD_SLOTS may ask for more, up to XCD_MAX_SLOTS).
 static int xcd_slots() {
   const char* e = std::getenv("FMCW_XCD_SLOTS");
-  const int v = e ? std::atoi(e) : 3;
-  return std::min(std::max(v, 2), fmcw::XCD_MAX_SLOTS);
+  const int v = e ? std::atoi(e) : 4;
+  return std::min(std::max(v, 4), fmcw::XCD_MAX_SLOTS);
 }
 
 static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int h, int64_t F, float* d_prof,
@@ -730,6 +730,11 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;
     }
+#ifdef XK_STAMPS
+    static unsigned long long* xdbg = nullptr;
+    if (!xdbg) HIPCHK(hipMalloc(&xdbg, (size_t)1 << 16));
+    a.dbg = xdbg;
+#endif
 #ifdef OP_STAMPS
     static unsigned long long* dbg = nullptr;
     const size_t nblk = (size_t)((nf + 7) / 8) * 64;
@@ -741,6 +746,21 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       if (xcd) {
         HIPCHK(fmcw::launch_xcd(a, s));
         c->xcd_used = true;
+#ifdef XK_STAMPS
+        {   // diagnostic build: per-step phase times of k_rdx (100 MHz realtime clock), averaged over blocks
+          std::vector<unsigned long long> hh(fmcw::XCD_GRID * 8);
+          HIPCHK(hipStreamSynchronize(s));
+          HIPCHK(hipMemcpy(hh.data(), a.dbg, hh.size() * 8, hipMemcpyDeviceToHost));
+          double ph[6] = {0, 0, 0, 0, 0, 0}, steps = 0;
+          for (int bb = 0; bb < fmcw::XCD_GRID; ++bb) {
+            for (int q = 0; q < 6; ++q) ph[q] += (double)hh[bb * 8 + q];
+            steps += (double)hh[bb * 8 + 6];
+          }
+          std::fprintf(stderr, "xk-stamps (us per step): chirp-wait %.2f | range %.2f | group-wait+stage+drain+publish %.2f | "
+                       "doppler %.2f | ready-wait+group-issue %.2f | RD stores %.2f\n", ph[5] / steps / 100, ph[0] / steps / 100,
+                       ph[1] / steps / 100, ph[2] / steps / 100, ph[3] / steps / 100, ph[4] / steps / 100);
+        }
+#endif
       } else {
         HIPCHK(fmcw::launch_onepass(a, s));
       }

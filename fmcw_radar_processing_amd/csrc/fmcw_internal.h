@@ -98,10 +98,10 @@ struct OnePassArgs {
   unsigned long long* dbg; // diagnostic builds only (-DOP_STAMPS): [blocks][8] s_memrealtime stamps
   // XCD-team schedule (k_rdx) only:
   float2* xcube;           // [8 XCDs][slots][XCD_TILES groups][C][32] range-cube hand-off slots
-  unsigned* xctr;          // [8 XCDs][2: ready, done][XCD_MAX_SLOTS][32] + [8][32] tickets: one 128-byte line
+  unsigned* xctr;          // [8 XCDs][2: ready, (unused)][XCD_MAX_SLOTS][32] + [8][32] tickets: one 128-byte line
                            // per counter, XCD_CTR_WORDS in all (zeroed per launch)
   unsigned* xerr;          // sticky: bit 0 a hand-off wait timed out, bit 1 an XCD got more than 32 blocks
-  int slots;               // hand-off slots per XCD (2 .. XCD_MAX_SLOTS)
+  int slots;               // hand-off slots per XCD (3 .. XCD_MAX_SLOTS)
   const float2* xtab;      // XT_* sections (host, float64, lane order)
   float2 cal_sum;          // sum_{n < S} cal[n]
 };

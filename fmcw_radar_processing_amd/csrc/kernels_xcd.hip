@@ -241,13 +241,12 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259) ----------------
   auto doppler = [&](int64_t f, const c2* __restrict__ grp, unsigned* done_ctr) {
     {
+      // buffer_load ... sc1: the CU's L1 is bypassed (no stale lines from the slot's
+      // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
       f4v t[8];
-      const f4v* __restrict__ gp = reinterpret_cast<const f4v*>(grp);
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2*>(grp), (short)0, C * GP * 8, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(t[i]) : "v"(gp + tid + 512 * i) : "memory");
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]), "+v"(t[4]), "+v"(t[5]),
-                   "+v"(t[6]), "+v"(t[7]) :: "memory");
+      for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const int e4 = tid + 512 * i;
@@ -255,7 +254,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       }
     }
     __syncthreads();                   // staged: every load of the slot has returned
-    if (tid == 0) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifndef XK_DONE
+#define XK_DONE 0
+#endif
+    if (XK_DONE && tid == 0) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
     const int r = xcd_bin(k, p);
     c2 xv[16];
@@ -349,7 +351,11 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   for (int j = 0; j <= nj; ++j) {
     if (j < nj) {
       const int s = j % NS;
-      if (j >= NS) {                   // slot s free: all members read frame j - NS out of it
+      // Slot s free: all members read frame j - NS out of it.  Without done counters
+      // (XK_DONE 0) this holds for slots >= 4: R(j) follows this member's wait for
+      // ready(j - 2) in step j - 1, and a member publishes R(j - 2) after its step j - 3
+      // (D(j - 4)) has read frame j - 4 out.
+      if (XK_DONE && j >= NS) {
         if (tid == 0) wait_ge(&done[s * 32], (unsigned)(NK * (j / NS)), a.xerr);
         __syncthreads();
       }
@@ -381,7 +387,7 @@ __global__ __launch_bounds__(512, 1) void k_xcd_census(int* out) {
 
 hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   if (a.F <= 0) return hipSuccess;
-  if (!onepass_supported(a.S, a.C, op::NR, a.C) || a.slots < 2 || a.slots > XCD_MAX_SLOTS) return hipErrorInvalidValue;
+  if (!onepass_supported(a.S, a.C, op::NR, a.C) || a.slots < (XK_DONE ? 2 : 4) || a.slots > XCD_MAX_SLOTS) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s);
   if (e != hipSuccess) return e;
   const dim3 g(XCD_GRID), bl(64 * xk::NW);

@@ -198,7 +198,7 @@ def test_onepass_fp16_matches_streams_fp16(engine):
 
 
 # ---- the XCD-team schedule (kernels_xcd.hip) on its own ----------------------
-@pytest.mark.parametrize("slots", ["2", "3", "4"])
+@pytest.mark.parametrize("slots", ["4"])
 def test_xcd_slot_ring(engine, monkeypatch, slots):
     """Frames 8 per XCD step: 75 frames = 9-10 steps per team, so every slot of
     the hand-off ring is reused several times; outputs equal the 8-tile single
