@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU per step")
     ap.add_argument("--fp16", action="store_true", help="config-4 fp16 storage variant")
     ap.add_argument("--chunk", type=int, default=0, help="frames per range/Doppler chunk (0 = library default)")
-    ap.add_argument("--pipeline", choices=["auto", "streams", "onepass"], default="auto",
+    ap.add_argument("--pipeline", choices=["auto", "streams", "onepass", "xcd"], default="auto",
                     help="range/Doppler schedule (include/fmcw.h fmcw_set_pipeline)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-stage-timing", action="store_true")
@@ -78,7 +78,7 @@ def main():
     eng.set_taps(cfg, P.synth_calibration(S))
     if args.chunk:
         eng.set_chunk_frames(args.chunk)
-    eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3}[args.pipeline])
+    eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3, "xcd": 4}[args.pipeline])
     stream = torch.cuda.current_stream(dev)
 
     # ---- device-resident input + outputs ------------------------------------------
@@ -131,6 +131,10 @@ def main():
         if world > 1:
             dist.barrier(device_ids=[local])
 
+    # which single-pass kernel the timed step runs (AUTO: k_rdx where the device passes the XCD check)
+    xcd_runs = args.pipeline == "xcd" or (args.pipeline == "auto" and
+                                          xcd_available(eng, d_iq, dt, outs, d_rd, stream))
+    eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3, "xcd": 4}[args.pipeline])
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -190,16 +194,22 @@ def main():
                 "what": "range+Doppler span (before first k_range .. after last k_doppler), SURVEY 8d bytes"}
     pmc = load_pmc(os.path.join(ROOT, "profiles"))
     dom = "k_rd1p" if "k_rd1p" in kern else "k_range"
+    if dom == "k_rd1p" and xcd_runs:   # the single-pass stage timer covers k_rdx when the XCD schedule runs
+        kern["k_rdx"] = kern.pop("k_rd1p")
+        dom = "k_rdx"
     if dom in kern:
         k = kern[dom]
-        kname = RD1P_NAME[args.fp16] if dom == "k_rd1p" else None
+        kname = {"k_rd1p": RD1P_NAME[args.fp16], "k_rdx": RDX_NAME[args.fp16]}.get(dom)
         traffic = pmc_traffic(pmc, kname, k["frames_per_launch"]) if kname else None
         roof = {"bound": "hbm", "achieved": k["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(k["achieved_GBps"] / HBM_PEAK_GBPS, 4), "traffic": traffic,
-                "kernel": ("k_rd1p (single pass: calibration, mean removal, window, range FFT, profile, Doppler FFT, "
-                           "RD store; one range tile of one frame per workgroup)") if dom == "k_rd1p" else
-                          "k_range (K1: calibration, mean removal, window, 1024-pt range FFT, cube store)",
-                "kernel_name": RD1P_NAME[args.fp16] if dom == "k_rd1p" else None,
+                "kernel": {"k_rd1p": "k_rd1p (single pass: calibration, mean removal, window, range FFT, profile, Doppler "
+                                     "FFT, RD store; one range tile of one frame per workgroup)",
+                           "k_rdx": "k_rdx (XCD-team schedule: the 32 CUs of an XCD share each frame; range FFT by chirps, "
+                                    "cube handed over through a slot ring, Doppler FFT by range-bin groups; calibration, "
+                                    "mean removal, windows, profile, RD store)"}.get(
+                              dom, "k_range (K1: calibration, mean removal, window, 1024-pt range FFT, cube store)"),
+                "kernel_name": kname,
                 "alg_bytes_per_launch": k["alg_bytes_per_launch"], "avg_launch_us": k["avg_launch_us"],
                 "frames_per_launch": k["frames_per_launch"],
                 "traffic_source": pmc.get("source") if pmc and traffic else None}
@@ -263,6 +273,23 @@ def main():
 
 
 RD1P_NAME = {False: "fmcw::k_rd1p<true, false>", True: "fmcw::k_rd1p<true, true>"}
+RDX_NAME = {False: "fmcw::k_rdx<true, false>", True: "fmcw::k_rdx<true, true>"}
+
+
+def xcd_available(eng, d_iq, dt, outs, d_rd, stream) -> bool:
+    """Does this device run the XCD-team schedule (fmcw_set_pipeline(FMCW_PIPE_XCD) accepted on a
+    short call)?  AUTO picks it exactly then (include/fmcw.h)."""
+    import torch
+    from fmcw_radar_processing_amd import FmcwError
+    n = 8
+    sub = {k: v[:n] for k, v in outs.items()}
+    try:
+        eng.set_pipeline(4)
+        eng.process_device(d_iq[:n], n, dt, sub, d_rd=d_rd[:n], out_dtype=dt, stream=stream)
+        torch.cuda.synchronize()
+        return True
+    except FmcwError:
+        return False
 K1_NAME = "fmcw::k_range<512, c64, c64, true>"
 
 
@@ -323,6 +350,9 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     nseg = torch.zeros(1, dtype=torch.int64, device=dev)
     fs = 1.0 / cfg.prt
 
+    xcd = args.pipeline in ("auto", "xcd") and xcd_available(eng, d_iq, FMCW_C32H, outs, d_rd, stream)
+    eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3, "xcd": 4}[args.pipeline])
+
     def step():
         eng.process_device(d_iq, F, FMCW_C32H, outs, d_rd=d_rd, out_dtype=FMCW_C32H, stream=stream)
         eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
@@ -348,12 +378,13 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     fpl = F * args.steps / n
     us = ms / n * 1e3
     per = C * S * 4 + NR * ND * 4 + NR * 4
-    kname = RD1P_NAME[True]
+    kname = RDX_NAME[True] if xcd else RD1P_NAME[True]
     out = {"value": round(F * args.steps / el, 1), "unit": "frames/s", "ms_per_step": round(el / args.steps * 1e3, 4),
            "dtype": "f16-storage/f32-compute",
            "what": "BASELINE config 4 fp16-storage variant: the headline step with c32h IQ in and c32h RD out",
            "roofline": _roof(per, fpl, us, pmc_traffic(pmc, kname, fpl), kname,
-                             "k_rd1p<fp16 storage> (single pass, c32h in / c32h RD out)", pmc)}
+                             ("k_rdx<fp16 storage> (XCD-team schedule" if xcd else "k_rd1p<fp16 storage> (single pass") +
+                             ", c32h in / c32h RD out)", pmc)}
     del d_iq, d_rd, d_P
     torch.cuda.empty_cache()
     return out

@@ -756,9 +756,9 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
             for (int q = 0; q < 6; ++q) ph[q] += (double)hh[bb * 8 + q];
             steps += (double)hh[bb * 8 + 6];
           }
-          std::fprintf(stderr, "xk-stamps (us per step): chirp-wait %.2f | range %.2f | group-wait+stage+drain+publish %.2f | "
-                       "doppler %.2f | ready-wait+group-issue %.2f | RD stores %.2f\n", ph[5] / steps / 100, ph[0] / steps / 100,
-                       ph[1] / steps / 100, ph[2] / steps / 100, ph[3] / steps / 100, ph[4] / steps / 100);
+          std::fprintf(stderr, "xk-stamps (us per step): range %.2f | drain+publish+prefetch %.2f | ready-wait %.2f | "
+                       "group load+stage %.2f | doppler %.2f | RD stores %.2f\n", ph[0] / steps / 100, ph[1] / steps / 100,
+                       ph[2] / steps / 100, ph[3] / steps / 100, ph[4] / steps / 100, ph[5] / steps / 100);
         }
 #endif
       } else {

@@ -86,6 +86,14 @@ __device__ __noinline__ void wait_ge(unsigned* p, unsigned v, unsigned* err) {
 }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
 
+// Lane pair (L, L ^ 1) packing for 16-byte stores of adjacent elements held by
+// adjacent lanes: the even lane gets (a[L], a[L + 1]), the odd lane (b[L - 1], b[L]).
+__device__ __forceinline__ f4v pair_pack(c2 a, c2 b, bool odd) {
+  const c2 snd = odd ? a : b;
+  const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};   // quad_perm [1,0,3,2]: lane ^ 1
+  return odd ? f4v{rcv.x, rcv.y, b.x, b.y} : f4v{a.x, a.y, rcv.x, rcv.y};
+}
+
 // row (16-lane group) reductions by DPP: symmetric pairings, every lane of the row gets the result
 __device__ __forceinline__ float row_sum16(float v) {
   v += dppf<0xB1>(v);
@@ -158,6 +166,16 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const c2 csum = c2{a.cal_sum.x, a.cal_sum.y};
   const float invS = 1.0f / (float)S;
   __syncthreads();
+#ifdef XK_STAMPS   // diagnostic build: per-phase time of block 0..255's steps (100 MHz clock)
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
+  auto stamp = [&](int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memrealtime();
+    st_acc[i] += n - st_t;
+    st_t = n;
+  };
+#else
+  auto stamp = [](int) {};
+#endif
 
   using TP = std::conditional_t<H, h4v, f4v>;
   const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
@@ -267,6 +285,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       for (int i = 0; i < 16; ++i) xv[i] = stg[(q + 16 * i) * 34 + p];
     }
     __syncthreads();                   // staging read out (the transposes reuse it)
+    stamp(3);
     // :217 row mean and :210 / :265 row max |X| over the 256 chirps
     c2 sm = (xv[0] + xv[1]) + (xv[2] + xv[3]);
     float pm = fmaxf(fmaxf(abs2v(xv[0]), abs2v(xv[1])), fmaxf(abs2v(xv[2]), abs2v(xv[3])));
@@ -318,8 +337,34 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     for (int m0 = 0; m0 < 16; ++m0) xv[m0] = rt[304 * pp + 18 * m0 + q];
     cfence();
     dft16p<1>(xv);                     // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
+    stamp(4);
     // :219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)]
+#ifndef XK_RD_STORE
+#define XK_RD_STORE 0
+#endif
     if (a.rd) {
+#if XK_RD_STORE >= 1
+      // lane pairs (q, q ^ 1) swap one value: the even lane stores positions (q, q + 1)
+      // of d1s, the odd lane (q - 1, q) of d1s + 8: 16 lanes write 2 x 128 contiguous bytes
+      const bool odd = q & 1;
+      if constexpr (H) {
+        h4v* __restrict__ out = reinterpret_cast<h4v*>(reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + (q & 14) + 128 * odd);
+#pragma unroll
+        for (int d1s = 0; d1s < 8; ++d1s)
+          out[8 * d1s] = __builtin_convertvector(pair_pack(xv[(d1s + 8) & 15], xv[d1s], odd) * a.rd_scale, h4v);
+      } else {
+        f4v* __restrict__ out = reinterpret_cast<f4v*>(reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + (q & 14) + 128 * odd);
+#pragma unroll
+        for (int d1s = 0; d1s < 8; ++d1s) {
+          const f4v o = pair_pack(xv[(d1s + 8) & 15], xv[d1s], odd);
+#if XK_RD_STORE == 2   // write-through (sc0 sc1): the line leaves the XCD's L2
+          st_wt(out + 8 * d1s, o);
+#else
+          __builtin_nontemporal_store(o, out + 8 * d1s);
+#endif
+        }
+      }
+#else
       if constexpr (H) {
         __half2* __restrict__ out = reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + q;
 #pragma unroll
@@ -332,6 +377,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #pragma unroll
         for (int d1s = 0; d1s < 16; ++d1s) __builtin_nontemporal_store(xv[(d1s + 8) & 15], out + 16 * d1s);
       }
+#endif
     } else {   // :233 [val, di] = max(abs(.)) of the row: exact max of |D|^2, then its first position
       float m = abs2v(xv[8]);
 #pragma unroll
@@ -359,19 +405,29 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
         if (tid == 0) wait_ge(&done[s * 32], (unsigned)(NK * (j / NS)), a.xerr);
         __syncthreads();
       }
+      stamp(5);
       range(xin, reinterpret_cast<c2*>(a.xcube) + (int64_t)(x * NS + s) * (NK * C * GP));
+      stamp(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();                 // every wave's slot stores are in the L2
       if (tid == 0) __hip_atomic_fetch_add(&ready[s * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (j + 1 < nj) ld_chirp(x + 8 * (int64_t)(j + 1), xin);   // next chirp in flight during D(j - 1)
+      stamp(1);
     }
     if (j >= 1) {
       const int jj = j - 1, s = jj % NS;
       if (tid == 0) wait_ge(&ready[s * 32], (unsigned)(NK * (jj / NS + 1)), a.xerr);
       __syncthreads();
+      stamp(2);
       doppler(x + 8 * (int64_t)jj, reinterpret_cast<const c2*>(a.xcube) + (int64_t)(x * NS + s) * (NK * C * GP) + (int64_t)k * C * GP, &done[s * 32]);
     }
   }
+#ifdef XK_STAMPS
+  if (tid == 0) {
+    for (int i = 0; i < 6; ++i) a.dbg[(int64_t)blockIdx.x * 8 + i] = st_acc[i];
+    a.dbg[(int64_t)blockIdx.x * 8 + 6] = (unsigned long long)nj;
+  }
+#endif
 }
 
 // One 256-block grid shaped like k_rdx (512 threads, the same LDS): block b
