@@ -68,6 +68,7 @@ struct LdsX {
   c2 twr2[15][64];
   c2 twd1[15][64];
   float wdl[16][64];                   // 2chebwin of chirp (l & 15) + 16 i
+  f4v cwp[16][64];                     // {cal w', w'} of sample 2 l + e + 128 i, index 2 i + e (w' = IF_scale 2blackman)
   float key[GP];                       // candidate key per group position (profile or -1)
 };
 
@@ -142,7 +143,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const int nj = a.F > x ? (int)((a.F - x + 7) / 8) : 0;   // frames x + 8 j of this XCD
   const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
   unsigned* ready = a.xctr + (x * 2 + 0) * 32 * XCD_MAX_SLOTS;
-  unsigned* done = a.xctr + (x * 2 + 1) * 32 * XCD_MAX_SLOTS;
 
   for (int i = tid; i < 44 * 64; i += 512) {
     const c2 v = tov(a.xtab[i]);
@@ -152,17 +152,11 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   }
   for (int i = tid; i < 16 * 64; i += 512) L.wdl[i >> 6][i & 63] = a.wd[(i & 15) + 16 * (i >> 6)];
   // :203-205 per-lane constants of samples n = 2 lane + e + 128 i: w' = IF_scale 2blackman, cal w'
-  float wp[16];
-  c2 cw[16];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int n = 2 * lane + e + 128 * i;
-      const float4 cv = n < S ? a.calw[n] : make_float4(0.f, 0.f, 0.f, 0.f);
-      wp[2 * i + e] = cv.z;
-      cw[2 * i + e] = c2{cv.x * cv.z, cv.y * cv.z};
-    }
+  for (int i = tid; i < 16 * 64; i += 512) {
+    const int l = i & 63, v = i >> 6, n = 2 * l + (v & 1) + 128 * (v >> 1);
+    const float4 cv = n < S ? a.calw[n] : make_float4(0.f, 0.f, 0.f, 0.f);
+    L.cwp[v][l] = f4v{cv.x * cv.z, cv.y * cv.z, cv.z, 0.f};
+  }
   const c2 csum = c2{a.cal_sum.x, a.cal_sum.y};
   const float invS = 1.0f / (float)S;
   __syncthreads();
@@ -207,7 +201,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     for (int n = 4; n < 16; n += 4) sm += (v[n] + v[n + 1]) + (v[n + 2] + v[n + 3]);
     const c2 mu = (wave_sum_c(sm) - csum) * invS;       // :204 mean of (x - cal) over the chirp
 #pragma unroll
-    for (int n = 0; n < 16; ++n) v[n] = __builtin_elementwise_fma(v[n] - mu, c2{wp[n], wp[n]}, -cw[n]);   // (x - cal - mu) w'
+    for (int n = 0; n < 16; ++n) {
+      const f4v cp = L.cwp[n][lane];
+      v[n] = __builtin_elementwise_fma(v[n] - mu, cp.zz, -cp.xy);   // (x - cal - mu) w'
+    }
     c2 z0[8], z1[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { z0[i] = v[2 * i]; z1[i] = v[2 * i + 1]; }
@@ -257,25 +254,22 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   };
 
   // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259) ----------------
-  auto doppler = [&](int64_t f, const c2* __restrict__ grp, unsigned* done_ctr) {
-    {
-      // buffer_load ... sc1: the CU's L1 is bypassed (no stale lines from the slot's
-      // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
-      f4v t[8];
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2*>(grp), (short)0, C * GP * 8, 0x00020000);
+  // buffer_load ... sc1: the CU's L1 is bypassed (no stale lines from the slot's
+  // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
+  auto ld_group = [&](const c2* __restrict__ grp, f4v (&t)[8]) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2*>(grp), (short)0, C * GP * 8, 0x00020000);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
+    for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
+  };
+  auto stage = [&](const f4v (&t)[8]) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int e4 = tid + 512 * i;
-        L.u.stg[(e4 >> 4) * 17 + (e4 & 15)] = t[i];
-      }
+    for (int i = 0; i < 8; ++i) {
+      const int e4 = tid + 512 * i;
+      L.u.stg[(e4 >> 4) * 17 + (e4 & 15)] = t[i];
     }
-    __syncthreads();                   // staged: every load of the slot has returned
-#ifndef XK_DONE
-#define XK_DONE 0
-#endif
-    if (XK_DONE && tid == 0) __hip_atomic_fetch_add(done_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  // D of one frame from its staged group (the caller staged it and synchronised)
+  auto doppler_staged = [&](int64_t f) {
     const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
     const int r = xcd_bin(k, p);
     c2 xv[16];
@@ -391,37 +385,75 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       if (q == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
     }
   };
+  [[maybe_unused]] auto doppler = [&](int64_t f, const c2* __restrict__ grp, unsigned*) {
+    f4v t[8];
+    ld_group(grp, t);
+    stage(t);
+    __syncthreads();                   // staged: every load of the slot has returned
+    doppler_staged(f);
+  };
 
+  c2* __restrict__ slots0 = reinterpret_cast<c2*>(a.xcube) + (int64_t)x * NS * (NK * C * GP);
+  auto slot = [&](int j) { return slots0 + (int64_t)(j % NS) * (NK * C * GP); };
+  auto frame = [&](int j) { return x + 8 * (int64_t)j; };
+  auto wait_ready = [&](int j) {       // every member published R(j)
+    if (tid == 0) wait_ge(&ready[(j % NS) * 32], (unsigned)(NK * (j / NS + 1)), a.xerr);
+    __syncthreads();
+  };
+  // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - NS,
+  // and R(j) runs after this member saw ready(j - 2); a member publishes R(j - 2)
+  // only after its own reads of frame j - 4 (at most) have returned, so slots >= 4.
   TP xin[8];
-  if (nj > 0) ld_chirp(x, xin);
+  if (nj > 0) ld_chirp(frame(0), xin);
+#ifndef XK_DEFER
+#define XK_DEFER 1
+#endif
+#if XK_DEFER
+  // Step j: the group of frame j - 2 (published a whole step ago, so the wait is
+  // short) is loaded first and lands under R(j); the drain of R(j)'s slot stores
+  // also covers it; it is staged before the next chirp's loads go out (so no wait
+  // on the group can also wait for them), then R(j) is published and D(j - 2) runs.
+  f4v grp[8];
+  for (int j = 0; j < nj + 2; ++j) {
+    const bool dj = j >= 2, rj = j < nj;
+    if (dj) {
+      wait_ready(j - 2);
+      ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
+    }
+    stamp(5);
+    if (rj) range(xin, slot(j));
+    stamp(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // slot stores in the L2, group in
+    __syncthreads();                   // (and the range transposes are free for the staging)
+    if (dj) stage(grp);
+    if (rj && tid == 0) __hip_atomic_fetch_add(&ready[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (j + 1 < nj) ld_chirp(frame(j + 1), xin);   // in flight during D(j - 2)
+    stamp(1);
+    if (dj) {
+      __syncthreads();                 // staged
+      stamp(2);
+      doppler_staged(frame(j - 2));
+    }
+  }
+#else
   for (int j = 0; j <= nj; ++j) {
     if (j < nj) {
-      const int s = j % NS;
-      // Slot s free: all members read frame j - NS out of it.  Without done counters
-      // (XK_DONE 0) this holds for slots >= 4: R(j) follows this member's wait for
-      // ready(j - 2) in step j - 1, and a member publishes R(j - 2) after its step j - 3
-      // (D(j - 4)) has read frame j - 4 out.
-      if (XK_DONE && j >= NS) {
-        if (tid == 0) wait_ge(&done[s * 32], (unsigned)(NK * (j / NS)), a.xerr);
-        __syncthreads();
-      }
       stamp(5);
-      range(xin, reinterpret_cast<c2*>(a.xcube) + (int64_t)(x * NS + s) * (NK * C * GP));
+      range(xin, slot(j));
       stamp(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();                 // every wave's slot stores are in the L2
-      if (tid == 0) __hip_atomic_fetch_add(&ready[s * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (j + 1 < nj) ld_chirp(x + 8 * (int64_t)(j + 1), xin);   // next chirp in flight during D(j - 1)
+      if (tid == 0) __hip_atomic_fetch_add(&ready[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (j + 1 < nj) ld_chirp(frame(j + 1), xin);   // next chirp in flight during D(j - 1)
       stamp(1);
     }
     if (j >= 1) {
-      const int jj = j - 1, s = jj % NS;
-      if (tid == 0) wait_ge(&ready[s * 32], (unsigned)(NK * (jj / NS + 1)), a.xerr);
-      __syncthreads();
+      wait_ready(j - 1);
       stamp(2);
-      doppler(x + 8 * (int64_t)jj, reinterpret_cast<const c2*>(a.xcube) + (int64_t)(x * NS + s) * (NK * C * GP) + (int64_t)k * C * GP, &done[s * 32]);
+      doppler(frame(j - 1), slot(j - 1) + (int64_t)k * C * GP, nullptr);
     }
   }
+#endif
 #ifdef XK_STAMPS
   if (tid == 0) {
     for (int i = 0; i < 6; ++i) a.dbg[(int64_t)blockIdx.x * 8 + i] = st_acc[i];
@@ -443,7 +475,7 @@ __global__ __launch_bounds__(512, 1) void k_xcd_census(int* out) {
 
 hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   if (a.F <= 0) return hipSuccess;
-  if (!onepass_supported(a.S, a.C, op::NR, a.C) || a.slots < (XK_DONE ? 2 : 4) || a.slots > XCD_MAX_SLOTS) return hipErrorInvalidValue;
+  if (!onepass_supported(a.S, a.C, op::NR, a.C) || a.slots < 4 || a.slots > XCD_MAX_SLOTS) return hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s);
   if (e != hipSuccess) return e;
   const dim3 g(XCD_GRID), bl(64 * xk::NW);
