@@ -87,6 +87,19 @@ __device__ __noinline__ void wait_ge(unsigned* p, unsigned v, unsigned* err) {
 }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
 
+// s_waitcnt vmcnt(n) for the counts the k_rdx step can have behind a store batch
+// (vmcnt needs an immediate); any other n waits for everything
+__device__ __forceinline__ void vm_wait_le(int n) {
+  switch (n) {
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
+    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
 // Lane pair (L, L ^ 1) packing for 16-byte stores of adjacent elements held by
 // adjacent lanes: the even lane gets (a[L], a[L + 1]), the odd lane (b[L - 1], b[L]).
 __device__ __forceinline__ f4v pair_pack(c2 a, c2 b, bool odd) {
@@ -406,9 +419,49 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   TP xin[8];
   if (nj > 0) ld_chirp(frame(0), xin);
 #ifndef XK_DEFER
-#define XK_DEFER 1
+#define XK_DEFER 2
 #endif
-#if XK_DEFER
+#if XK_DEFER == 2
+  // Step j: R(j - 1) is published first, its slot stores having drained under
+  // D(j - 3) (vmcnt counts the operations issued after them: the chirp loads, the
+  // profile store, the RD stores); then the group of frame j - 2 is loaded, R(j)
+  // runs while it lands, the group is staged once it is in (vmcnt(16): only R(j)'s
+  // slot stores behind it), the next chirp's loads go out and D(j - 2) runs.
+  // (first and last two steps peeled: in the steady loop the body is straight-line,
+  // so the compiler's own wait before the staging counts R(j)'s 16 slot stores)
+  auto body = [&](int j, bool dj, bool rj, bool pub) {
+    f4v grp[8];
+    if (pub) {
+      const int after = (j < nj ? 8 : 0) + (j - 1 >= 2 ? 1 + (a.rd ? 16 : 1) : 0);
+      vm_wait_le(after);
+      __syncthreads();                 // every wave's slot stores of R(j - 1) are in the L2
+      if (tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (dj) {
+      wait_ready(j - 2);
+      ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
+    }
+    stamp(5);
+    if (rj) range(xin, slot(j));
+    stamp(0);
+    if (rj) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the group is in (R(j)'s slot stores may not be)
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();                   // the range transposes are free for the staging
+    if (dj) stage(grp);
+    cfence();
+    if (j + 1 < nj) ld_chirp(frame(j + 1), xin);   // in flight during D(j - 2)
+    stamp(1);
+    if (dj) {
+      __syncthreads();                 // staged
+      stamp(2);
+      doppler_staged(frame(j - 2));
+    }
+  };
+  int j = 0;
+  for (; j < 2 && j < nj + 2; ++j) body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj);
+  for (; j < nj; ++j) body(j, true, true, true);
+  for (; j < nj + 2; ++j) body(j, true, false, j - 1 < nj);
+#elif XK_DEFER
   // Step j: the group of frame j - 2 (published a whole step ago, so the wait is
   // short) is loaded first and lands under R(j); the drain of R(j)'s slot stores
   // also covers it; it is staged before the next chirp's loads go out (so no wait
