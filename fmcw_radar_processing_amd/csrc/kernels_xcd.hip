@@ -14,21 +14,20 @@
 //                       windows, runs 32 Doppler FFTs and writes its RD rows.
 //
 // So each input byte is read once, and the cube (2 MiB per frame) makes one
-// trip through the XCD's L2 instead of eight re-reads of the frame.  One
+// trip through the XCD instead of eight L2 re-reads of the frame.  One
 // persistent 512-thread workgroup per CU; the 32 blocks that land on XCD x
 // (HW_REG_XCC_ID; xcd_census checks the 32-per-XCD deal before the schedule is
-// enabled) form its team, members k = 0..31 by ticket, and take frames x + 8 j.  Step
-// j runs R(j) then D(j-1), so the slot of frame j-1 is complete (all 32
-// members published) before anyone reads it; a ring of `slots` slots per XCD
-// with ready / done counters keeps a member from overwriting a slot that is
-// still being read.
+// enabled) form its team, members k = 0..31 by ticket, and take frames x + 8 j.
+// Step j publishes R(j-1), runs R(j) and D(j-2) (the Doppler two steps behind,
+// see the step loop); a ring of `slots` (4) slots per XCD with one ready
+// counter each: D(j-2) starts when all 32 members published frame j-2.
 //
 // Hand-off protocol (tools/xcd_probe.hip measured it at 0.99 M frames/s of
 // pure data movement): producers store the slot with plain stores (the lines
-// stay in the XCD's L2), `s_waitcnt vmcnt(0)` in every wave, a workgroup
-// barrier, then one agent-scope atomic add on the slot's ready counter.
-// Consumers poll with relaxed agent loads (global_load sc1), then read the
-// slot with sc1 loads, which bypass the CU's L1 and are served by the XCD's L2.
+// stay in the XCD's L2), `s_waitcnt vmcnt` in every wave, a workgroup barrier,
+// then one agent-scope atomic add on the slot's ready counter.  Consumers poll
+// with relaxed agent loads (global_load sc1), then read the slot with
+// buffer_load sc1, which bypasses the CU's L1 and is served by the XCD's L2.
 // Producer and consumer are on the same XCD, so no L2 write-back is needed.
 // Every wait is bounded: a timeout sets xerr bit 0 and lets the grid drain.
 //
@@ -100,13 +99,6 @@ __device__ __forceinline__ void vm_wait_le(int n) {
   }
 }
 
-// Lane pair (L, L ^ 1) packing for 16-byte stores of adjacent elements held by
-// adjacent lanes: the even lane gets (a[L], a[L + 1]), the odd lane (b[L - 1], b[L]).
-__device__ __forceinline__ f4v pair_pack(c2 a, c2 b, bool odd) {
-  const c2 snd = odd ? a : b;
-  const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};   // quad_perm [1,0,3,2]: lane ^ 1
-  return odd ? f4v{rcv.x, rcv.y, b.x, b.y} : f4v{a.x, a.y, rcv.x, rcv.y};
-}
 
 // row (16-lane group) reductions by DPP: symmetric pairings, every lane of the row gets the result
 __device__ __forceinline__ float row_sum16(float v) {
@@ -346,32 +338,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     dft16p<1>(xv);                     // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
     stamp(4);
     // :219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)]
-#ifndef XK_RD_STORE
-#define XK_RD_STORE 0
-#endif
     if (a.rd) {
-#if XK_RD_STORE >= 1
-      // lane pairs (q, q ^ 1) swap one value: the even lane stores positions (q, q + 1)
-      // of d1s, the odd lane (q - 1, q) of d1s + 8: 16 lanes write 2 x 128 contiguous bytes
-      const bool odd = q & 1;
-      if constexpr (H) {
-        h4v* __restrict__ out = reinterpret_cast<h4v*>(reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + (q & 14) + 128 * odd);
-#pragma unroll
-        for (int d1s = 0; d1s < 8; ++d1s)
-          out[8 * d1s] = __builtin_convertvector(pair_pack(xv[(d1s + 8) & 15], xv[d1s], odd) * a.rd_scale, h4v);
-      } else {
-        f4v* __restrict__ out = reinterpret_cast<f4v*>(reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + (q & 14) + 128 * odd);
-#pragma unroll
-        for (int d1s = 0; d1s < 8; ++d1s) {
-          const f4v o = pair_pack(xv[(d1s + 8) & 15], xv[d1s], odd);
-#if XK_RD_STORE == 2   // write-through (sc0 sc1): the line leaves the XCD's L2
-          st_wt(out + 8 * d1s, o);
-#else
-          __builtin_nontemporal_store(o, out + 8 * d1s);
-#endif
-        }
-      }
-#else
       if constexpr (H) {
         __half2* __restrict__ out = reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + q;
 #pragma unroll
@@ -384,7 +351,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #pragma unroll
         for (int d1s = 0; d1s < 16; ++d1s) __builtin_nontemporal_store(xv[(d1s + 8) & 15], out + 16 * d1s);
       }
-#endif
     } else {   // :233 [val, di] = max(abs(.)) of the row: exact max of |D|^2, then its first position
       float m = abs2v(xv[8]);
 #pragma unroll
@@ -397,13 +363,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       e = row_min16(e);
       if (q == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
     }
-  };
-  [[maybe_unused]] auto doppler = [&](int64_t f, const c2* __restrict__ grp, unsigned*) {
-    f4v t[8];
-    ld_group(grp, t);
-    stage(t);
-    __syncthreads();                   // staged: every load of the slot has returned
-    doppler_staged(f);
   };
 
   c2* __restrict__ slots0 = reinterpret_cast<c2*>(a.xcube) + (int64_t)x * NS * (NK * C * GP);
@@ -418,10 +377,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // only after its own reads of frame j - 4 (at most) have returned, so slots >= 4.
   TP xin[8];
   if (nj > 0) ld_chirp(frame(0), xin);
-#ifndef XK_DEFER
-#define XK_DEFER 2
-#endif
-#if XK_DEFER == 2
   // Step j: R(j - 1) is published first, its slot stores having drained under
   // D(j - 3) (vmcnt counts the operations issued after them: the chirp loads, the
   // profile store, the RD stores); then the group of frame j - 2 is loaded, R(j)
@@ -461,52 +416,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   for (; j < 2 && j < nj + 2; ++j) body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj);
   for (; j < nj; ++j) body(j, true, true, true);
   for (; j < nj + 2; ++j) body(j, true, false, j - 1 < nj);
-#elif XK_DEFER
-  // Step j: the group of frame j - 2 (published a whole step ago, so the wait is
-  // short) is loaded first and lands under R(j); the drain of R(j)'s slot stores
-  // also covers it; it is staged before the next chirp's loads go out (so no wait
-  // on the group can also wait for them), then R(j) is published and D(j - 2) runs.
-  f4v grp[8];
-  for (int j = 0; j < nj + 2; ++j) {
-    const bool dj = j >= 2, rj = j < nj;
-    if (dj) {
-      wait_ready(j - 2);
-      ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
-    }
-    stamp(5);
-    if (rj) range(xin, slot(j));
-    stamp(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // slot stores in the L2, group in
-    __syncthreads();                   // (and the range transposes are free for the staging)
-    if (dj) stage(grp);
-    if (rj && tid == 0) __hip_atomic_fetch_add(&ready[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (j + 1 < nj) ld_chirp(frame(j + 1), xin);   // in flight during D(j - 2)
-    stamp(1);
-    if (dj) {
-      __syncthreads();                 // staged
-      stamp(2);
-      doppler_staged(frame(j - 2));
-    }
-  }
-#else
-  for (int j = 0; j <= nj; ++j) {
-    if (j < nj) {
-      stamp(5);
-      range(xin, slot(j));
-      stamp(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();                 // every wave's slot stores are in the L2
-      if (tid == 0) __hip_atomic_fetch_add(&ready[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (j + 1 < nj) ld_chirp(frame(j + 1), xin);   // next chirp in flight during D(j - 1)
-      stamp(1);
-    }
-    if (j >= 1) {
-      wait_ready(j - 1);
-      stamp(2);
-      doppler(frame(j - 1), slot(j - 1) + (int64_t)k * C * GP, nullptr);
-    }
-  }
-#endif
 #ifdef XK_STAMPS
   if (tid == 0) {
     for (int i = 0; i < 6; ++i) a.dbg[(int64_t)blockIdx.x * 8 + i] = st_acc[i];
