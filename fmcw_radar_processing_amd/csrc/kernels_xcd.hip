@@ -283,8 +283,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) xv[i] = stg[(q + 16 * i) * 34 + p];
     }
-    __syncthreads();                   // staging read out (the transposes reuse it)
-    stamp(3);
     // :217 row mean and :210 / :265 row max |X| over the 256 chirps
     c2 sm = (xv[0] + xv[1]) + (xv[2] + xv[3]);
     float pm = fmaxf(fmaxf(abs2v(xv[0]), abs2v(xv[1])), fmaxf(abs2v(xv[2]), abs2v(xv[3])));
@@ -302,7 +300,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       const double rng = (double)r * a.dist_per_bin;
       L.key[p] = (r >= 1 && r <= NR - 2 && rng >= a.min_d && rng <= a.max_d && pr > a.range_thr) ? pr : -1.f;
     }
-    __syncthreads();                   // keys of all 32 rows
+    __syncthreads();                   // keys of all 32 rows in; staging read out (the transposes reuse it)
+    stamp(3);
     {   // slow-time candidates (:257-259): the XCD_CAND strongest in-window rows of the group
       float kv = lane < GP ? L.key[lane] : -1.f;
       const int ki = xcd_bin(k, lane & (GP - 1));
@@ -368,10 +367,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   c2* __restrict__ slots0 = reinterpret_cast<c2*>(a.xcube) + (int64_t)x * NS * (NK * C * GP);
   auto slot = [&](int j) { return slots0 + (int64_t)(j % NS) * (NK * C * GP); };
   auto frame = [&](int j) { return x + 8 * (int64_t)j; };
-  auto wait_ready = [&](int j) {       // every member published R(j)
-    if (tid == 0) wait_ge(&ready[(j % NS) * 32], (unsigned)(NK * (j / NS + 1)), a.xerr);
-    __syncthreads();
-  };
   // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - NS,
   // and R(j) runs after this member saw ready(j - 2); a member publishes R(j - 2)
   // only after its own reads of frame j - 4 (at most) have returned, so slots >= 4.
@@ -386,16 +381,13 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // so the compiler's own wait before the staging counts R(j)'s 16 slot stores)
   auto body = [&](int j, bool dj, bool rj, bool pub) {
     f4v grp[8];
-    if (pub) {
-      const int after = (j < nj ? 8 : 0) + (j - 1 >= 2 ? 1 + (a.rd ? 16 : 1) : 0);
-      vm_wait_le(after);
-      __syncthreads();                 // every wave's slot stores of R(j - 1) are in the L2
-      if (tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (dj) {
-      wait_ready(j - 2);
-      ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
-    }
+    // one barrier for both: after it every wave's slot stores of R(j - 1) are in the
+    // L2 (publish) and tid 0 has seen every member's R(j - 2) (the group may be read)
+    if (pub) vm_wait_le((j < nj ? 8 : 0) + (j - 1 >= 2 ? 1 + (a.rd ? 16 : 1) : 0));
+    if (dj && tid == 0) wait_ge(&ready[((j - 2) % NS) * 32], (unsigned)(NK * ((j - 2) / NS + 1)), a.xerr);
+    if (pub || dj) __syncthreads();
+    if (pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dj) ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
     stamp(5);
     if (rj) range(xin, slot(j));
     stamp(0);
