@@ -47,6 +47,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 
 namespace fmcw {
 namespace xk {
@@ -427,11 +428,31 @@ __global__ __launch_bounds__(512, 1) void k_xcd_census(int* out) {
   }
 }
 
+// k_rdx needs all 256 of its workgroups resident together (team members wait for
+// each other), so two of its launches must never share a device at the same time:
+// launches from different streams (several contexts over one device, host threads)
+// are chained on the device through one event per device.  (Another process's
+// persistent kernel on the same GPU is not covered; the bounded waits then report
+// FMCW_E_HIP instead of hanging.)
+namespace {
+std::mutex xcd_chain_mu;
+hipEvent_t xcd_chain_ev[64] = {};
+}  // namespace
+
 hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   if (a.F <= 0) return hipSuccess;
   if (!onepass_supported(a.S, a.C, op::NR, a.C) || a.slots < 4 || a.slots > XCD_MAX_SLOTS) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  std::lock_guard<std::mutex> lk(xcd_chain_mu);
+  if (!xcd_chain_ev[dev]) {
+    if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
+  } else if ((e = hipStreamWaitEvent(s, xcd_chain_ev[dev], 0)) != hipSuccess) {
+    return e;
+  }
+  if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   const dim3 g(XCD_GRID), bl(64 * xk::NW);
   if (a.S == op::NR) {
     if (a.h) hipLaunchKernelGGL((k_rdx<true, true>), g, bl, 0, s, a);
@@ -440,7 +461,8 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
     if (a.h) hipLaunchKernelGGL((k_rdx<false, true>), g, bl, 0, s, a);
     else hipLaunchKernelGGL((k_rdx<false, false>), g, bl, 0, s, a);
   }
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return hipEventRecord(xcd_chain_ev[dev], s);
 }
 
 hipError_t xcd_census(int* ok) {
