@@ -11,7 +11,15 @@ STFT halo, global max and range_speed gather run as RCCL collectives.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--fp16]
 
-Rank 0 prints one JSON line (contract in the task statement).
+--gpus N > 1 without a torchrun environment starts N ranks itself (a child
+torch.distributed.run, before any GPU call) and exits with its status; under
+torchrun the world size must equal --gpus.
+
+Rank 0 prints one JSON line (contract in the task statement).  After every
+timed region it checks the launches' sticky error word (fmcw_synchronize) and,
+in the oracle leg at the end (CPU baseline), compares every timed frame's
+outputs with the float64 C oracle (oracle/fmcw_oracle.c): the "checked" key.
+A failed check still prints the line, then exits non-zero.
 """
 from __future__ import annotations
 
@@ -48,11 +56,56 @@ def parse():
                     help="skip the extra single-GPU lines (fp16 storage, config 2, host-pointer path)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-pointer path line (profile runs: its small launches share kernel names)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the full-size comparison with the C oracle (profile runs)")
+    ap.add_argument("--dry-dist", action="store_true",
+                    help="launcher test without a GPU: the ranks meet over gloo and rank 0 prints n_gpus")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` outside torchrun: one rank per GPU through a child
+    torch.distributed.run on 127.0.0.1 (this process never touches the GPU, so no
+    exec of a GPU-initialised process); returns the launcher's exit status."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_dist(args, world: int, rank: int) -> None:
+    """The launcher path on CPU (tests/test_bench_launch.py): ranks meet over gloo."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "ranks_reduced": int(t.item()), "dry_dist": True}),
+              flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if args.dry_dist:
+        return dry_dist(args, world, rank)
     import torch
     import torch.distributed as dist
 
@@ -61,8 +114,6 @@ def main():
     from fmcw_radar_processing_amd import params as P
     from fmcw_radar_processing_amd.engine import Engine
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -138,6 +189,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    sticky_check(eng, "warmup")
     # level 2: HIP events around every K1/K2/K3 launch on its own stream (the
     # per-kernel roofline below) plus the range+Doppler span and STFT launches
     level = 0 if args.no_stage_timing else 2
@@ -153,6 +205,7 @@ def main():
     elapsed = time.perf_counter() - t0
     stages = eng.timing_read() if level else {}
     eng.timing(0)
+    sticky_check(eng, "timed steps")          # a timed-out k_rdx hand-off invalidates the run
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -233,16 +286,26 @@ def main():
                   "GBps_root_egress": round(world * nf * C * S * esz / ft / 1e9, 1)}
         del src, dst
 
-    extra = {}
+    extra, legs = {}, []
+    if rank == 0 and not args.no_check:
+        legs.append(dict(name="config4_f32" if not args.fp16 else "config4_fp16", cfg=cfg, d_iq=d_iq, outs=outs,
+                         d_rd=d_rd, d_db=d_P, d_nseg=nseg, fp16=args.fp16, world=world))
     if world == 1 and not args.no_extras and not args.fp16:
-        del d_rd, d_P
-        extra["fp16_storage"] = bench_fp16(eng, cfg, F, args, dev, stream, pmc)
-        extra["config2_range_fft"] = bench_config2(eng, args, dev, stream, pmc)
+        extra["fp16_storage"], leg16 = bench_fp16(eng, cfg, F, args, dev, stream, pmc)
+        extra["config2_range_fft"], leg2 = bench_config2(eng, args, dev, stream, pmc)
+        if not args.no_check:
+            legs += [leg16, leg2]
         if not args.no_host_path:
             extra["host_path"] = bench_host_path(eng)
         eng.set_taps(cfg, P.synth_calibration(S))
+    checked, ok = None, True
     if rank == 0:
-        cpu = cpu_baseline(args.cpu_seconds, d_iq, F, dt) if args.cpu_seconds > 0 else None
+        # oracle leg, after every timed region: the CPU baseline on this run's own frames and the
+        # full-size comparison of every timed frame's outputs with the float64 C oracle
+        cpu = cpu_baseline(args.cpu_seconds, d_iq, F, dt) if args.cpu_seconds > 0 and not legs else None
+        if legs:
+            checked, cpu = oracle_leg(legs, args.cpu_seconds)
+            ok = all(v.get("pass", False) for v in checked.values())
         total_frames = world * F * args.steps
         value = total_frames / elapsed
         line = {
@@ -261,6 +324,7 @@ def main():
             "path_roofline": path,
             "kernels": kern,
             "cpu_baseline": cpu,
+            "checked": checked,
             "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items() if v[1]},
             "frames_with_target": det,
         }
@@ -269,7 +333,22 @@ def main():
         line.update(extra)
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier(device_ids=[local])
         dist.destroy_process_group()
+    if not ok:
+        print("bench.py: the full-size check against the oracle FAILED (see \"checked\")", file=sys.stderr, flush=True)
+        sys.exit(1)
+
+
+def sticky_check(eng, where: str) -> None:
+    """fmcw_synchronize: raises when a k_rdx hand-off wait of any launch since the
+    last check timed out (its outputs are invalid); the bench then exits non-zero."""
+    from fmcw_radar_processing_amd import FmcwError
+    try:
+        eng.synchronize()
+    except FmcwError as e:
+        print(f"bench.py: {where}: {e}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 RD1P_NAME = {False: "fmcw::k_rd1p<true, false>", True: "fmcw::k_rd1p<true, true>"}
@@ -287,6 +366,7 @@ def xcd_available(eng, d_iq, dt, outs, d_rd, stream) -> bool:
         eng.set_pipeline(4)
         eng.process_device(d_iq[:n], n, dt, sub, d_rd=d_rd[:n], out_dtype=dt, stream=stream)
         torch.cuda.synchronize()
+        eng.synchronize()                 # the launch's hand-offs completed (sticky error word clear)
         return True
     except FmcwError:
         return False
@@ -365,6 +445,7 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
+    sticky_check(eng, "fp16 warmup")
     eng.timing(2)
     eng.timing_reset()
     t0 = time.perf_counter()
@@ -374,6 +455,7 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     el = time.perf_counter() - t0
     st = eng.timing_read()
     eng.timing(0)
+    sticky_check(eng, "fp16 timed steps")
     ms, n = st["onepass"]
     fpl = F * args.steps / n
     us = ms / n * 1e3
@@ -385,9 +467,9 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
            "roofline": _roof(per, fpl, us, pmc_traffic(pmc, kname, fpl), kname,
                              ("k_rdx<fp16 storage> (XCD-team schedule" if xcd else "k_rd1p<fp16 storage> (single pass") +
                              ", c32h in / c32h RD out)", pmc)}
-    del d_iq, d_rd, d_P
-    torch.cuda.empty_cache()
-    return out
+    leg = dict(name="config4_fp16", cfg=cfg, d_iq=d_iq, outs=outs, d_rd=d_rd, d_db=d_P, d_nseg=nseg, fp16=True,
+               world=1)
+    return out, leg
 
 
 def bench_config2(eng, args, dev, stream, pmc):
@@ -421,9 +503,8 @@ def bench_config2(eng, args, dev, stream, pmc):
            "dtype": "f32", "what": "BASELINE config 2: 4096 x 128 x 512 IQ, range FFT only, cube + profile written",
            "roofline": _roof(per, F2, us, pmc_traffic(pmc, K1_NAME, F2), K1_NAME,
                              "K1 k_range (calibration, mean, window, 512-pt range FFT, cube + profile store)", pmc)}
-    del d_iq, d_cube, d_prof
-    torch.cuda.empty_cache()
-    return out
+    leg = dict(name="config2", cfg=cfg2, d_iq=d_iq, d_cube=d_cube, d_prof=d_prof)
+    return out, leg
 
 
 def json_timing(sp, python: bool):
@@ -497,33 +578,177 @@ def bench_host_path(eng):
     return res
 
 
-def cpu_baseline(budget_s: float, d_iq, F: int, dt: int):
+def _oracle_setup(cfg):
+    """The float64 oracle's parameters, windows and calibration for a bench config
+    (the same taps the bench gave the device: cfg windows, SURVEY 8d calibration)."""
+    from fmcw_radar_processing_amd import params as P
+    from oracle import oracle as O
+    p = O.derive_params(P.deployed_device(cfg.nts, cfg.pn), nr=cfg.nr, nd=cfg.nd, parity=False)
+    wr, wd = O.windows(cfg.nts, cfg.pn)
+    return p, wr, wd, P.synth_calibration(cfg.nts)
+
+
+def _host_frames(d_iq, f0: int, f1: int, C: int, S: int):
+    """Frames f0..f1 of a device IQ tensor as complex64 (fp16 storage: the same values widened)."""
+    x = d_iq[f0:f1].float().cpu().numpy()
+    return x.view(np.float32).reshape(f1 - f0, C, S, 2).view(np.complex64)[..., 0]
+
+
+def _rel_rows(got, ref):
+    got = np.asarray(got, np.float64)
+    num = np.sqrt(np.sum((got - ref) ** 2, axis=1))
+    return num / np.maximum(np.sqrt(np.sum(ref ** 2, axis=1)), 1e-300)
+
+
+def check_rd_leg(leg, threads: int):
+    """Every frame of a config-4 step (radar_processing.m:203-219, :257-283) against the C
+    oracle: RD map per-frame relative L2 (raw, and relaxed as tests/helpers.rd_rel_err),
+    profile, detections (exact except near-ties), slow-time rows, and the hop-1 STFT dB.
+    Returns (result dict, seconds of oracle_process, frames, seconds of the oracle STFT)."""
+    from oracle import coracle as CO
+    from oracle import oracle as O
+    cfg, fp16, world = leg["cfg"], leg["fp16"], leg.get("world", 1)
+    C, S, NR, ND = cfg.pn, cfg.nts, cfg.nr, cfg.nd
+    d_iq = leg["d_iq"]
+    F = d_iq.shape[0]
+    p, wr, wd, cal = _oracle_setup(cfg)
+    B = max(16, 4 * threads)
+    rd_buf = np.zeros((B, NR, ND), np.complex128)
+    keys = ("profile", "tgt_count", "tgt_range_idx", "tgt_range_mag", "tgt_doppler_idx", "slow_mag")
+    per = {k: [] for k in keys}
+    raw, rlx = np.zeros(F), np.zeros(F)
+    busy = 0.0
+    for f0 in range(0, F, B):
+        f1 = min(F, f0 + B)
+        n = f1 - f0
+        iq = _host_frames(d_iq, f0, f1, C, S)
+        t = time.perf_counter()
+        out = CO.process_frames(iq, cal, p, wr, wd, rd_out=rd_buf[:n], nthreads=threads, want_pre=True)
+        busy += time.perf_counter() - t
+        g = leg["d_rd"][f0:f1]
+        unscale = 1.0
+        if fp16:                       # c32h RD holds D / (Nr Nd) (include/fmcw.h)
+            g, unscale = g.float(), float(NR * ND)
+        num, den = CO.err2(rd_buf[:n], g.cpu().numpy(), unscale, threads)
+        raw[f0:f1] = np.sqrt(num / np.maximum(den, 1e-300))
+        rlx[f0:f1] = np.sqrt(num) / np.maximum(np.maximum(np.sqrt(den), 0.1 * np.sqrt(out["pre"])), 1e-300)
+        for k in keys:
+            per[k].append(out[k])
+    ref = {k: np.concatenate(v) for k, v in per.items()}
+    got = {k: leg["outs"][k].cpu().numpy() for k in keys}
+    srt = np.sort(ref["profile"], axis=1)
+    tie = (srt[:, -1] - srt[:, -2]) <= 1e-5 * srt[:, -1]       # frames whose top-2 bins are within 1e-5
+    differ = np.zeros(F, bool)
+    for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
+        a, b = got[k].reshape(F, -1), ref[k].reshape(F, -1)
+        differ |= np.any(a != b, axis=1)
+    bad_det = int(np.sum(differ & ~tie))
+    has = ref["tgt_count"] > 0
+    prof_err = float(_rel_rows(got["profile"], ref["profile"]).max())
+    slow_err = float(_rel_rows(got["slow_mag"][has], ref["slow_mag"][has]).max()) if has.any() else 0.0
+    slow_zero = bool(np.all(got["slow_mag"][~has & ~differ] == 0))
+    m = ref["tgt_count"][:, None] > np.arange(ref["tgt_range_mag"].shape[1])[None, :]
+    mag_err = float(np.max(np.abs(got["tgt_range_mag"][m] - ref["tgt_range_mag"][m]) / ref["tgt_range_mag"][m])) \
+        if m.any() else 0.0
+    # :270-283 STFT dB of the concatenated slow-time signal, on the native nfft/2+1 bins
+    x = ref["slow_mag"][has].reshape(-1)
+    t = time.perf_counter()
+    sp = CO.spectrogram(x, cfg.prt, O.stft_window("hann"), STFT_NOVERLAP, STFT_NFFT, nbins=0, nthreads=threads)
+    t_stft = time.perf_counter() - t
+    nref = sp["intensity"].shape[0]
+    nc = min(int(leg["d_nseg"].item()), nref)
+    if differ.any():                   # compare the segments before the first frame whose detection differs
+        fd = int(np.argmax(differ))
+        nc = min(nc, C * int(np.sum(has[:fd])) - (STFT_WLEN - 1))
+    db_tol, db_floor = (0.05, -60.0) if fp16 else (1e-3, -80.0)
+    stft_err = None
+    if nc > 0:
+        g = leg["d_db"][:nc].cpu().numpy().astype(np.float64)
+        r = sp["intensity"][:nc]
+        if world > 1:                  # rank 0's dB is normalised by the global max(P): renormalise both locally
+            g, r = g - g.max(), r - r.max()
+        sel = r > db_floor
+        stft_err = float(np.max(np.abs(g[sel] - r[sel]))) if sel.any() else 0.0
+    rd_tol = 3e-3 if fp16 else 1e-5
+    res = {"frames": F, "what": "every frame of the last timed step vs oracle/fmcw_oracle.c (fp64)",
+           "rd_rel_l2_raw_max": float(raw.max()), "rd_rel_l2_raw_median": float(np.median(raw)),
+           "rd_rel_l2_relaxed_max": float(rlx.max()), "rd_tol": rd_tol,
+           "profile_rel_l2_max": prof_err, "slow_rows_rel_l2_max": slow_err, "range_mag_rel_max": mag_err,
+           "row_tol": 1e-5, "detections_differing": bad_det, "near_tie_frames": int(tie.sum()),
+           "frames_with_target": int(has.sum()), "no_target_rows_zero": slow_zero,
+           "stft_segments_compared": int(max(nc, 0)), "stft_segments_ref": int(nref),
+           "stft_max_abs_db": stft_err, "stft_tol_db": db_tol, "stft_db_floor": db_floor}
+    res["pass"] = bool(raw.max() <= rd_tol and prof_err <= 1e-5 and slow_err <= 1e-5 and mag_err <= 1e-5 and
+                       bad_det == 0 and slow_zero and stft_err is not None and stft_err <= db_tol and
+                       nc >= 0.99 * nref - world * STFT_WLEN)
+    return res, busy, F, t_stft
+
+
+def check_cube_leg(leg, threads: int):
+    """Config 2 (range FFT only, :203-207, :210): every frame's range cube (per-frame
+    relative L2) and profile against the C oracle."""
+    from oracle import coracle as CO
+    cfg = leg["cfg"]
+    C, S, NR = cfg.pn, cfg.nts, cfg.nr
+    d_iq = leg["d_iq"]
+    F = d_iq.shape[0]
+    p, wr, wd, cal = _oracle_setup(cfg)
+    B = max(16, 4 * threads)
+    cube_buf = np.zeros((B, C, NR), np.complex128)
+    err, prof = np.zeros(F), []
+    for f0 in range(0, F, B):
+        f1 = min(F, f0 + B)
+        n = f1 - f0
+        out = CO.process_frames(_host_frames(d_iq, f0, f1, C, S), cal, p, wr, wd, cube_out=cube_buf[:n],
+                                nthreads=threads)
+        num, den = CO.err2(cube_buf[:n], leg["d_cube"][f0:f1].cpu().numpy(), 1.0, threads)
+        err[f0:f1] = np.sqrt(num / np.maximum(den, 1e-300))
+        prof.append(out["profile"])
+    perr = float(_rel_rows(leg["d_prof"].cpu().numpy(), np.concatenate(prof)).max())
+    res = {"frames": F, "what": "every frame of the last timed launch vs oracle/fmcw_oracle.c (fp64)",
+           "cube_rel_l2_max": float(err.max()), "cube_rel_l2_median": float(np.median(err)),
+           "profile_rel_l2_max": perr, "tol": 1e-5}
+    res["pass"] = bool(err.max() <= 1e-5 and perr <= 1e-5)
+    return res
+
+
+def oracle_leg(legs, budget_s: float):
+    """After every timed region (rank 0): the full-size check of each leg, and the CPU
+    baseline, whose first pass is the headline leg's own check pass."""
+    cores, _ = host_cores()
+    checked, cpu = {}, None
+    for leg in legs:
+        if "d_cube" in leg:
+            checked[leg["name"]] = check_cube_leg(leg, cores)
+            continue
+        res, busy, nfr, t_stft = check_rd_leg(leg, cores)
+        checked[leg["name"]] = res
+        if cpu is None and budget_s > 0:
+            cpu = cpu_baseline(budget_s, leg["d_iq"], leg["d_iq"].shape[0], None, prior=(nfr, busy + t_stft))
+    return checked, cpu
+
+
+def cpu_baseline(budget_s: float, d_iq, F: int, dt, prior=None):
     """C restatement of radar_processing.m:197-299 (oracle/fmcw_oracle.c, fp64,
     OpenMP over frames) on a bounded sample of the SAME device-resident frames
     (copied back in batches), on this host's cores.  Every row's Doppler FFT is
-    computed (as the GPU path does), then the hop-1 STFT of the slow-time signal."""
-    import torch
-    from fmcw_radar_processing_amd import params as P
+    computed (as the GPU path does), then the hop-1 STFT of the slow-time signal.
+    prior = (frames, seconds) already measured on all cores (the check pass)."""
     from oracle import coracle as CO
     from oracle import oracle as O
+    from fmcw_radar_processing_amd import params as P
     cores, host = host_cores()
     cfg = P.config(4)
-    p = O.derive_params(P.deployed_device(cfg.nts, cfg.pn), nr=cfg.nr, nd=cfg.nd, parity=False)
-    wr, wd = O.windows(cfg.nts, cfg.pn)
-    cal = P.synth_calibration(cfg.nts)
+    p, wr, wd, cal = _oracle_setup(cfg)
     win = O.stft_window("hann")
     B = 4 * cores
 
-    def batch(f0):
-        x = d_iq[f0:f0 + B].float().cpu().numpy()            # fp16 storage: the same values widened
-        return x.view(np.float32).reshape(x.shape[0], cfg.pn, cfg.nts, 2).view(np.complex64)[..., 0]
-
-    def run(threads, budget):
-        done, slow, busy = 0, [], 0.0
+    def run(threads, budget, done=0, busy=0.0):
+        slow = []
         rd = np.zeros((B, cfg.nr, cfg.nd), np.complex128)
         f0 = 0
         while busy < budget or done < B:
-            iq = batch(f0)                                      # not timed
+            iq = _host_frames(d_iq, f0, min(F, f0 + B), cfg.pn, cfg.nts)      # not timed
             t = time.perf_counter()
             out = CO.process_frames(iq, cal, p, wr, wd, rd_out=rd[:iq.shape[0]], nthreads=threads)
             keep = out["tgt_count"] > 0
@@ -532,16 +757,18 @@ def cpu_baseline(budget_s: float, d_iq, F: int, dt: int):
             done += iq.shape[0]
             f0 = (f0 + B) % max(F - B, 1)
         t = time.perf_counter()
-        x = np.concatenate(slow)
+        x = np.concatenate(slow) if slow else np.zeros(0)
         if len(x) >= STFT_WLEN:
             CO.spectrogram(x, cfg.prt, win, STFT_NOVERLAP, STFT_NFFT, nbins=0, nthreads=threads)
         return done / (busy + time.perf_counter() - t), done
 
-    v_all, n_all = run(cores, budget_s)
+    n0, s0 = prior if prior else (0, 0.0)
+    v_all, n_all = run(cores, budget_s, done=n0, busy=s0)
     v_one, n_one = run(1, max(2.0, budget_s / 4))
     return {"value": round(v_all, 2), "unit": "frames/s", "cores": cores, "kind": "port",
             "sample": f"{n_all} config-4 frames (the bench's own device frames, copied back) through "
-                      f"oracle/fmcw_oracle.c (fp64, OpenMP {cores} threads, every RD row) + hop-1 STFT nfft 64",
+                      f"oracle/fmcw_oracle.c (fp64, OpenMP {cores} threads, every RD row) + hop-1 STFT nfft 64"
+                      + (f"; the first {n0} are the full-size check pass" if n0 else ""),
             "single_thread": {"value": round(v_one, 2), "frames": n_one}, "host": host}
 
 

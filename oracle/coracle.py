@@ -23,6 +23,10 @@ def lib():
         P = ct.c_void_p
         _lib.oracle_process.argtypes = [ct.c_int] * 6 + [ct.c_double] * 6 + [P] * 4 + [ct.c_int64] + [P] * 8 + [ct.c_int]
         _lib.oracle_process.restype = ct.c_int
+        _lib.oracle_process2.argtypes = [ct.c_int] * 6 + [ct.c_double] * 6 + [P] * 4 + [ct.c_int64] + [P] * 9 + [ct.c_int]
+        _lib.oracle_process2.restype = ct.c_int
+        _lib.oracle_err2.argtypes = [P, P, ct.c_double, ct.c_int64, ct.c_int64, P, P, ct.c_int]
+        _lib.oracle_err2.restype = None
         _lib.oracle_stft.argtypes = [P, ct.c_int64, P, ct.c_int, ct.c_int, ct.c_int, ct.c_double, ct.c_int, P, P, P,
                                      ct.c_int]
         _lib.oracle_stft.restype = ct.c_int64
@@ -34,9 +38,12 @@ def _p(a):
     return ct.c_void_p(0) if a is None else ct.c_void_p(a.ctypes.data)
 
 
-def process_frames(iq, cal, p, wr, wd, want_cube=False, want_rd=False, nthreads=0, rd_out=None):
-    """rd_out: preallocated complex128 [F][nr][nd] that receives every row's
-    Doppler spectrum (no allocation per call; used by bench.py's CPU baseline)."""
+def process_frames(iq, cal, p, wr, wd, want_cube=False, want_rd=False, nthreads=0, rd_out=None, cube_out=None,
+                   want_pre=False):
+    """rd_out / cube_out: preallocated complex128 [F][nr][nd] / [F][C][nr] that
+    receive every row's Doppler spectrum / the range cube (no allocation per call;
+    used by bench.py's CPU baseline and full-size check).  want_pre: also return
+    'pre' [F], the energy entering the Doppler FFT (relaxed RD normalisation)."""
     iq = np.ascontiguousarray(iq, np.complex64)
     F, C, S = iq.shape
     nr, nd, M = p["nr"], p["nd"], p["max_targets"]
@@ -47,21 +54,42 @@ def process_frames(iq, cal, p, wr, wd, want_cube=False, want_rd=False, nthreads=
     if rd_out is not None:
         assert rd_out.dtype == np.complex128 and rd_out.shape == (F, nr, nd) and rd_out.flags.c_contiguous
         rd = rd_out
+    if cube_out is not None:
+        assert cube_out.dtype == np.complex128 and cube_out.shape == (F, C, nr) and cube_out.flags.c_contiguous
+        cube = cube_out
+    pre = np.zeros(F) if want_pre else None
     c = np.ascontiguousarray(np.asarray(cal, np.complex128))
     wr = np.ascontiguousarray(wr, np.float64)
     wd = np.ascontiguousarray(wd, np.float64)
-    st = lib().oracle_process(S, C, nr, nd, M, int(p["doppler_fallback_idx"]), p["if_scale"], p["range_thr"],
-                              p["doppler_thr"], p["min_d"], p["max_d"], p["dist_per_bin"], _p(wr), _p(wd), _p(c),
-                              _p(iq), F, _p(out["profile"]), _p(out["tgt_count"]), _p(out["tgt_range_idx"]),
-                              _p(out["tgt_range_mag"]), _p(out["tgt_doppler_idx"]), _p(out["slow_mag"]), _p(cube),
-                              _p(rd), int(nthreads))
+    st = lib().oracle_process2(S, C, nr, nd, M, int(p["doppler_fallback_idx"]), p["if_scale"], p["range_thr"],
+                               p["doppler_thr"], p["min_d"], p["max_d"], p["dist_per_bin"], _p(wr), _p(wd), _p(c),
+                               _p(iq), F, _p(out["profile"]), _p(out["tgt_count"]), _p(out["tgt_range_idx"]),
+                               _p(out["tgt_range_mag"]), _p(out["tgt_doppler_idx"]), _p(out["slow_mag"]), _p(cube),
+                               _p(rd), _p(pre), int(nthreads))
     if st != 0:
         raise RuntimeError("oracle_process failed")
-    if want_cube:
+    if want_cube or cube_out is not None:
         out["cube"] = cube
-    if want_rd:
+    if want_rd or rd_out is not None:
         out["rd"] = rd
+    if want_pre:
+        out["pre"] = pre
     return out
+
+
+def err2(ref, got, unscale=1.0, nthreads=0):
+    """Per-frame (sum |got*unscale - ref|^2, sum |ref|^2): ref complex128 [F][...],
+    got complex64 (or float32 [..][2]) of the same shape."""
+    ref = np.ascontiguousarray(ref, np.complex128)
+    got = np.ascontiguousarray(got)
+    if got.dtype == np.complex64:
+        got = got.view(np.float32)
+    assert got.dtype == np.float32 and got.size == 2 * ref.size
+    F = ref.shape[0]
+    n = ref.size // max(F, 1)
+    num, den = np.zeros(F), np.zeros(F)
+    lib().oracle_err2(_p(ref), _p(got), float(unscale), F, n, _p(num), _p(den), int(nthreads))
+    return num, den
 
 
 def spectrogram(x, prt, win, noverlap, nfft, nbins=1024, nthreads=0):

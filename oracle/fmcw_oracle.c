@@ -79,8 +79,8 @@ int oracle_num_threads(void) {
 static void one_frame(int S, int C, int Nr, int Nd, int M, int fallback, double if_scale, double thr_r,
                       double thr_d, double min_d, double max_d, double dpb, const double* wr, const double* wd,
                       const double* cal, const float* iq, double* prof, int32_t* count, int32_t* ridx,
-                      double* rmag, int32_t* didx, double* slow, double* cube, double* rd, cd* X, cd* row,
-                      const plan_t* pr, const plan_t* pd) {
+                      double* rmag, int32_t* didx, double* slow, double* cube, double* rd, double* pre, cd* X,
+                      cd* row, const plan_t* pr, const plan_t* pd) {
   const int nmax = S < Nr ? S : Nr;
   for (int k = 0; k < C; ++k) {                       /* :203-205 */
     const float* x = iq + (size_t)k * S * 2;
@@ -102,6 +102,16 @@ static void one_frame(int S, int C, int Nr, int Nd, int M, int fallback, double 
     fft_inplace(Xk, pr);
   }
   if (cube) memcpy(cube, X, sizeof(cd) * (size_t)C * Nr);
+  if (pre) {   /* energy entering the Doppler FFT before the :218 mean removal, Nd * sum |X w|^2 */
+    const int kq = C < Nd ? C : Nd;
+    double e = 0;
+    for (int k = 0; k < kq; ++k)
+      for (int r = 0; r < Nr; ++r) {
+        const cd v = X[(size_t)k * Nr + r];
+        e += (v.re * v.re + v.im * v.im) * wd[k] * wd[k];
+      }
+    *pre = Nd * e;
+  }
   /* rows are gathered RB at a time (RB*16 B contiguous per chirp) */
   enum { RB = 8 };
   cd* rows = row;   /* scratch [RB][max(C, Nd)] */
@@ -180,11 +190,13 @@ static void one_frame(int S, int C, int Nr, int Nd, int M, int fallback, double 
   for (int k = 0; k < C; ++k) slow[k] = n > 0 ? cabs_(X[(size_t)k * Nr + sel[0]]) : 0.0;   /* :259 */
 }
 
-/* iq: [F][C][S] complex float32 interleaved.  Outputs [F]-major like libfmcw. */
-int oracle_process(int S, int C, int Nr, int Nd, int M, int fallback, double if_scale, double thr_r,
-                   double thr_d, double min_d, double max_d, double dpb, const double* wr, const double* wd,
-                   const double* cal, const float* iq, int64_t F, double* prof, int32_t* count, int32_t* ridx,
-                   double* rmag, int32_t* didx, double* slow, double* cube, double* rd, int nthreads) {
+/* iq: [F][C][S] complex float32 interleaved.  Outputs [F]-major like libfmcw.
+ * pre (optional, [F]): Nd * sum |X w_d|^2 per frame, the normalisation floor of
+ * the relaxed RD error (tests/helpers.py rd_rel_err). */
+int oracle_process2(int S, int C, int Nr, int Nd, int M, int fallback, double if_scale, double thr_r,
+                    double thr_d, double min_d, double max_d, double dpb, const double* wr, const double* wd,
+                    const double* cal, const float* iq, int64_t F, double* prof, int32_t* count, int32_t* ridx,
+                    double* rmag, int32_t* didx, double* slow, double* cube, double* rd, double* pre, int nthreads) {
   if (M < 1 || M > 8) return -1;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -201,8 +213,8 @@ int oracle_process(int S, int C, int Nr, int Nd, int M, int fallback, double if_
       one_frame(S, C, Nr, Nd, M, fallback, if_scale, thr_r, thr_d, min_d, max_d, dpb, wr, wd, cal,
                 iq + (size_t)f * C * S * 2, prof + (size_t)f * Nr, count + f, ridx + (size_t)f * M,
                 rmag + (size_t)f * M, didx + (size_t)f * M, slow + (size_t)f * C,
-                cube ? cube + (size_t)f * C * Nr * 2 : NULL, rd ? rd + (size_t)f * Nr * Nd * 2 : NULL, X, row,
-                &pr, &pd);
+                cube ? cube + (size_t)f * C * Nr * 2 : NULL, rd ? rd + (size_t)f * Nr * Nd * 2 : NULL,
+                pre ? pre + f : NULL, X, row, &pr, &pd);
     }
     free(X);
     free(row);
@@ -210,6 +222,38 @@ int oracle_process(int S, int C, int Nr, int Nd, int M, int fallback, double if_
     plan_free(&pd);
   }
   return 0;
+}
+
+int oracle_process(int S, int C, int Nr, int Nd, int M, int fallback, double if_scale, double thr_r,
+                   double thr_d, double min_d, double max_d, double dpb, const double* wr, const double* wd,
+                   const double* cal, const float* iq, int64_t F, double* prof, int32_t* count, int32_t* ridx,
+                   double* rmag, int32_t* didx, double* slow, double* cube, double* rd, int nthreads) {
+  return oracle_process2(S, C, Nr, Nd, M, fallback, if_scale, thr_r, thr_d, min_d, max_d, dpb, wr, wd, cal, iq, F,
+                         prof, count, ridx, rmag, didx, slow, cube, rd, NULL, nthreads);
+}
+
+/* Per-frame squared error of a device result against the float64 oracle:
+ * num2[f] = sum |got * unscale - ref|^2, den2[f] = sum |ref|^2 over the n complex
+ * values of frame f (got: complex float32 interleaved).  The bench's full-size
+ * check (bench.py) uses it on every frame it times. */
+void oracle_err2(const double* ref, const float* got, double unscale, int64_t F, int64_t n, double* num2,
+                 double* den2, int nthreads) {
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(static)
+#endif
+  for (int64_t f = 0; f < F; ++f) {
+    const double* r = ref + (size_t)f * n * 2;
+    const float* g = got + (size_t)f * n * 2;
+    double a = 0, b = 0;
+    for (int64_t i = 0; i < 2 * n; ++i) {
+      const double d = (double)g[i] * unscale - r[i];
+      a += d * d;
+      b += r[i] * r[i];
+    }
+    num2[f] = a;
+    den2[f] = b;
+  }
 }
 
 /* :270-299.  x real [L]; nfft power of two >= wlen; nlog = 0 -> dB on the native
