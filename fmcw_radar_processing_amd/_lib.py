@@ -45,7 +45,7 @@ class JsonField(ct.Structure):
                 ("rows", ct.c_int64), ("cols", ct.c_int64), ("row_stride", ct.c_int64), ("col_stride", ct.c_int64)]
 
 
-FMCW_JSON_STRING, FMCW_JSON_F32, FMCW_JSON_F64, FMCW_JSON_I32 = 0, 1, 2, 3
+FMCW_JSON_STRING, FMCW_JSON_F32, FMCW_JSON_F64, FMCW_JSON_I32, FMCW_JSON_BOOL = 0, 1, 2, 3, 4
 
 _P = ct.c_void_p
 _I32, _I64, _F, _D = ct.c_int32, ct.c_int64, ct.c_float, ct.c_double
@@ -56,6 +56,7 @@ SIGNATURES = {
     "fmcw_abi_version": (_I32, []),
     "fmcw_last_error": (ct.c_char_p, []),
     "fmcw_device_count": (ct.c_int, [ct.POINTER(_I32)]),
+    "fmcw_default_devices": (ct.c_int, [_I32, ct.POINTER(_I32), ct.POINTER(_I32)]),
     "fmcw_ctx_create": (ct.c_int, [_I32, ct.POINTER(_I32), ct.POINTER(_P)]),
     "fmcw_ctx_destroy": (ct.c_int, [_P]),
     "fmcw_ctx_devices": (ct.c_int, [_P, ct.POINTER(_I32), ct.POINTER(_I32), ct.POINTER(_I32)]),

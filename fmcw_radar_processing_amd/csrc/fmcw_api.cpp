@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -199,7 +200,25 @@ struct fmcw_ctx {
   hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out, s_bins;
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
-  DevBuf s_tab;                                // STFT 20-tap table W[nfft/2+1][20]
+  // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one: device calls on
+  // different streams (with different windows or nfft) never share a table
+  struct StreamTab {
+    hipStream_t s;
+    DevBuf t;
+  };
+  std::vector<std::unique_ptr<StreamTab>> s_tabs;
+  float2* stft_tab(hipStream_t st, size_t bytes, int* status) {
+    StreamTab* e = nullptr;
+    for (auto& x : s_tabs)
+      if (x->s == st) e = x.get();
+    if (!e) {
+      s_tabs.push_back(std::make_unique<StreamTab>());
+      e = s_tabs.back().get();
+      e->s = st;
+    }
+    *status = e->t.ensure(bytes);
+    return e->t.as<float2>();
+  }
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
@@ -376,6 +395,40 @@ int fmcw_device_count(int32_t* n) {
     return fail(FMCW_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
   }
   *n = d;
+  return FMCW_OK;
+}
+
+int fmcw_default_devices(int32_t cap, int32_t* ids, int32_t* n) {
+  if (!ids || !n || cap < 1) return fail(FMCW_E_ARG, "ids/n NULL or cap < 1");
+  *n = 0;
+  int nd = 0;
+  hipError_t e = hipGetDeviceCount(&nd);
+  if (e != hipSuccess) return fail(FMCW_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  const char* env = std::getenv("FMCW_DEVICES");
+  std::string v = env ? env : "";
+  v.erase(std::remove_if(v.begin(), v.end(), [](char ch) { return ch == ' ' || ch == '\t'; }), v.end());
+  if (v.empty() || v == "all") {
+    if (nd < 1) return fail(FMCW_E_HIP, "no HIP device present");
+    const int m = std::min<int>(nd, cap);
+    for (int i = 0; i < m; ++i) ids[i] = i;
+    *n = m;
+    return FMCW_OK;
+  }
+  int32_t m = 0;
+  size_t pos = 0;
+  while (pos <= v.size()) {
+    const size_t end = std::min(v.find(',', pos), v.size());
+    const std::string tok = v.substr(pos, end - pos);
+    char* stop = nullptr;
+    const long id = tok.empty() ? -1 : std::strtol(tok.c_str(), &stop, 10);
+    if (tok.empty() || *stop != '\0') return fail(FMCW_E_ARG, "FMCW_DEVICES: malformed list '" + v + "'");
+    if (id < 0 || id >= nd)
+      return fail(FMCW_E_ARG, "FMCW_DEVICES: device " + tok + " not present (" + std::to_string(nd) + " devices)");
+    if (m >= cap) return fail(FMCW_E_ARG, "FMCW_DEVICES: more ids than cap");
+    ids[m++] = (int32_t)id;
+    pos = end + 1;
+  }
+  *n = m;
   return FMCW_OK;
 }
 
@@ -1057,9 +1110,11 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
   a.max_seg = max_seg; a.P = d_P; a.pmax = d_pmax; a.nseg_out = d_nseg;
   StageTimer tm(c, 4, s);
   if (fmcw::stft_fast_path(wlen, a.hop)) {        // the reference's 20-tap window: W table + k_stft20
-    CHK(c->s_tab.ensure((size_t)(nfft / 2 + 1) * 20 * 8));
-    HIPCHK(fmcw::launch_stft_table(d_win, nfft, c->s_tab.as<float2>(), s));
-    HIPCHK(fmcw::launch_stft20(a, c->s_tab.as<float2>(), d_P ? 0 : 1, nullptr, s));
+    int st = FMCW_OK;
+    float2* tab = c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
+    CHK(st);
+    HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
+    HIPCHK(fmcw::launch_stft20(a, tab, d_P ? 0 : 1, nullptr, s));
   } else {
     HIPCHK(fmcw::launch_stft_power(a, s));
   }
@@ -1089,9 +1144,11 @@ int fmcw_stft_db_direct_device(fmcw_ctx* c, const float* d_slow, const int32_t* 
   a.inv_fs = (float)(1.0 / fs);
   a.max_seg = max_seg; a.P = nullptr; a.pmax = const_cast<float*>(d_pmax); a.nseg_out = nullptr;
   StageTimer tm(c, 5, s);
-  CHK(c->s_tab.ensure((size_t)(nfft / 2 + 1) * 20 * 8));
-  HIPCHK(fmcw::launch_stft_table(d_win, nfft, c->s_tab.as<float2>(), s));
-  HIPCHK(fmcw::launch_stft20(a, c->s_tab.as<float2>(), 2, d_out, s));
+  int st = FMCW_OK;
+  float2* tab = c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
+  CHK(st);
+  HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
+  HIPCHK(fmcw::launch_stft20(a, tab, 2, d_out, s));
   tm.done();
   return FMCW_OK;
 }
@@ -1307,7 +1364,10 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       a.pn = (int32_t)Ld; a.win = d->s_win.as<float>(); a.wlen = wlen; a.hop = hop; a.nfft = nf;
       a.inv_fs = (float)(1.0 / fs); a.max_seg = ns; a.bins = d->s_bins.as<int32_t>(); a.ncol = ncolP;
       StageTimer tm(d, 4, s);
-      HIPCHK(fmcw::launch_stft20(a, d->s_tab.as<float2>(), 3, d->s_P.as<float>(), s));
+      int st = FMCW_OK;
+      float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table on s
+      CHK(st);
+      HIPCHK(fmcw::launch_stft20(a, tab, 3, d->s_P.as<float>(), s));
       tm.done();
     }
     HIPCHK(hipStreamSynchronize(s));   // the host-side scalars above go out of scope

@@ -39,6 +39,18 @@ double elem(const fmcw_json_field& f, int64_t i, int64_t j) {
 }
 
 // one number as matlab_json._num formats it
+inline char* put_num(char* p, double v);
+
+// one element: a logical prints as true / false (MATLAB jsonencode of a logical array)
+inline char* put_elem(char* p, const fmcw_json_field& f, int64_t i, int64_t j) {
+  if (f.kind == FMCW_JSON_BOOL) {
+    const bool b = static_cast<const uint8_t*>(f.data)[i * f.row_stride + j * f.col_stride] != 0;
+    std::memcpy(p, b ? "true" : "false", b ? 4 : 5);
+    return p + (b ? 4 : 5);
+  }
+  return put_num(p, elem(f, i, j));
+}
+
 inline char* put_num(char* p, double v) {
   if (std::isnan(v) || std::isinf(v)) {
     std::memcpy(p, "null", 4);
@@ -95,7 +107,7 @@ void format_piece(Piece& pc, bool pretty) {
       if (e > pc.e0) lit(sep, nsep);
       if (pretty) lit(in1.data(), in1.size());
     }
-    p = put_num(p, elem(f, i, j));
+    p = put_elem(p, f, i, j);
     if (pc.matrix && j == C - 1) {        // close row i
       if (pretty) {
         lit("\n", 1);
@@ -129,7 +141,8 @@ int fmcw_json_write(const char* path, const fmcw_json_field* fields, int32_t n_f
     if (!f.name) return jfail(FMCW_E_ARG, "field " + std::to_string(k) + " has no name");
     if (f.kind == FMCW_JSON_STRING) {
       if (!f.data) return jfail(FMCW_E_ARG, std::string("string field '") + f.name + "' is NULL");
-    } else if (f.kind == FMCW_JSON_F32 || f.kind == FMCW_JSON_F64 || f.kind == FMCW_JSON_I32) {
+    } else if (f.kind == FMCW_JSON_F32 || f.kind == FMCW_JSON_F64 || f.kind == FMCW_JSON_I32 ||
+               f.kind == FMCW_JSON_BOOL) {
       if (f.rows < 0 || f.cols < 0 || (f.rows * f.cols > 0 && !f.data))
         return jfail(FMCW_E_ARG, std::string("bad array field '") + f.name + "'");
     } else {
@@ -158,7 +171,7 @@ int fmcw_json_write(const char* path, const fmcw_json_field* fields, int32_t n_f
       g += "[]";
     } else if (n == 1) {
       char buf[48];
-      g.append(buf, put_num(buf, elem(f, 0, 0)) - buf);
+      g.append(buf, put_elem(buf, f, 0, 0) - buf);
     } else {
       const bool matrix = f.rows > 1 && f.cols > 1;
       g += pp ? "[\n" : "[";

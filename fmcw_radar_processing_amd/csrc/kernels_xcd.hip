@@ -31,6 +31,17 @@
 // Producer and consumer are on the same XCD, so no L2 write-back is needed.
 // Every wait is bounded: a timeout sets xerr bit 0 and lets the grid drain.
 //
+// Reference chirp (static-target cancellation, :204 / :217-218).  Every chirp
+// except chirp 0 is transformed as the difference x_k - x_0 from the frame's
+// chirp 0 (loaded by every member into LDS): X'_k = FFT((d_k - mean d_k) w'),
+// d_k = x_k - x_0, so X_k = X'_k + X_0 by linearity, and the slot holds X_0 for
+// chirp 0 and X'_k for the others.  The Doppler stage forms the row mean from
+// the X'_k (X'_0 = 0), so a static target -- a component identical in every
+// chirp, removed by the :218 mean -- cancels in the time domain, before any
+// rounding of its large FFT values; the profile and the slow-time rows use
+// X_k = X'_k + X_0.  Without it the fp32 RD map of a static-target frame is off
+// by ~2.5e-5 of the frame's (small, cancelled) norm; with it every frame meets
+// the 1e-5 bar of SURVEY 8d.
 // Range FFT of one chirp in one wave (n = a + 128 i, r = k1 + 8 (s1 + 16 s2),
 // a = a0 + 8 a1):  lane l holds samples n = 2l + e + 128 i (8 16-byte loads);
 //   stage 1: DFT8 over i of both a = 2l + e, twiddle W1024^(a k1);
@@ -53,10 +64,22 @@ namespace fmcw {
 namespace xk {
 using namespace op;
 
+#ifdef XK_NOREF
+#define XK_REF 0
+#else
+#define XK_REF 1
+#endif
+#if defined(XK_RD16)
+#define XK_RD_STORES 8                 // RD stores per lane and row group (16-byte lane-pair stores)
+#else
+#define XK_RD_STORES 16
+#endif
 constexpr int NK = 32;                 // team members (CUs) per XCD
 constexpr int C = 256;                 // chirps = Doppler points
 constexpr int NW = 8;                  // waves per workgroup = chirps per member
 constexpr int GP = 32;                 // bins per group
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));
 static_assert(NK * NW == C && NK * GP == NR && NK == XCD_TILES, "team geometry");
 
 struct LdsX {
@@ -70,34 +93,43 @@ struct LdsX {
   float wdl[16][64];                   // 2chebwin of chirp (l & 15) + 16 i
   f4v cwp[16][64];                     // {cal w', w'} of sample 2 l + e + 128 i, index 2 i + e (w' = IF_scale 2blackman)
   float key[GP];                       // candidate key per group position (profile or -1)
+#ifndef XK_NOREF
+  f4v x0[512];                         // the frame's reference chirp (chirp 0) as loaded, c64 pairs (fp16: widened)
+#endif
 };
 
-__device__ __forceinline__ unsigned ld_flag(unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Poll of a hand-off counter: a scalar load that misses the scalar cache (glc: served by
+// the L2, where the agent-scope adds land).  It counts on lgkmcnt, not vmcnt, so the
+// polling wave's vector loads and stores stay in flight (a vector poll, or a call, would
+// make it wait for all of them first).  The value is waited for inside the asm.
+__device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+  unsigned v;
+  asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  return v;
 }
-// Bounded wait for *p >= v (one lane).  ~1 s before giving up; once any wait of
-// the launch timed out, the others return at once so the grid drains.
-__device__ __noinline__ void wait_ge(unsigned* p, unsigned v, unsigned* err) {
+// Bounded wait for *p >= v (wave-uniform).  ~1 s before giving up; once any wait of
+// the launch timed out (its abort word, zeroed per launch), the others return at
+// once so the grid drains.  The timeout is also or-ed into the sticky error word
+// that fmcw_synchronize reports; a later launch is not affected by it.  Inlined:
+// no call (a call waits for every outstanding memory operation of the wave).
+__device__ __forceinline__ void wait_ge(const unsigned* p, unsigned v, unsigned* abort, unsigned* err) {
   for (int it = 0; it < (1 << 20); ++it) {
     if (ld_flag(p) >= v) return;
-    if ((it & 63) == 63 && ld_flag(err)) return;
+    if ((it & 63) == 63 && ld_flag(abort)) return;
     __builtin_amdgcn_s_sleep(2);
   }
-  atomicOr(err, 1u);
+  if (threadIdx.x == 0) {
+    atomicOr(abort, 1u);
+    atomicOr(err, 1u);
+  }
 }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
 
-// s_waitcnt vmcnt(n) for the counts the k_rdx step can have behind a store batch
-// (vmcnt needs an immediate); any other n waits for everything
-__device__ __forceinline__ void vm_wait_le(int n) {
-  switch (n) {
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
-    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
-    case 17: asm volatile("s_waitcnt vmcnt(17)" ::: "memory"); break;
-    case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
+// s_waitcnt vmcnt(N) for a compile-time N (the k_rdx publish counts; tools/check_vmcnt.py
+// proves them on the built code)
+template <int N> __device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 
@@ -123,7 +155,9 @@ __device__ __forceinline__ int row_min16(int v) {
 
 }  // namespace xk
 
-template <bool FULL, bool H>   // H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic
+// H: fp16 storage (c32h IQ in, c32h RD out), fp32 arithmetic; RD: the RD map is written
+// (else only the row peaks), a template flag so that every hand-off wait count is static
+template <bool FULL, bool H, bool RD>
 __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   using namespace xk;
   __shared__ __attribute__((aligned(16))) LdsX L;
@@ -139,7 +173,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const int xx = (int)(xcc & 7);
     const int kk = (int)__hip_atomic_fetch_add(a.xctr + XCD_TICKETS + xx * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (kk >= NK) atomicOr(a.xerr, 2u);
+    if (kk >= NK) { atomicOr(a.xerr, 2u); atomicOr(a.xctr + XCD_ABORT, 1u); }
     team[0] = xx;
     team[1] = kk;
   }
@@ -150,6 +184,28 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
   unsigned* ready = a.xctr + (x * 2 + 0) * 32 * XCD_MAX_SLOTS;
 
+  using TP = std::conditional_t<H, h4v, f4v>;
+  const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
+#ifndef XK_NOREF
+  // the reference chirp (chirp 0) of the next frame: one sample pair per thread, loaded one
+  // step ahead (before the chirp loads, so the step's vmcnt counts cover it) and put into LDS
+  // before the barrier that opens the step
+  TP x0n{};
+  auto ld_ref = [&](int64_t f) __attribute__((always_inline)) {
+    const TP* __restrict__ q = iq + f * C * (int64_t)S2;
+    if constexpr (FULL) x0n = __builtin_nontemporal_load(q + tid);
+    else x0n = __builtin_nontemporal_load(q + (tid < S2 ? tid : 0));
+  };
+  auto put_ref = [&]() __attribute__((always_inline)) {
+    f4v t;
+    if constexpr (H) t = __builtin_convertvector(x0n, f4v);
+    else t = x0n;
+    if constexpr (!FULL)
+      if (tid >= S2) t = f4v{0.f, 0.f, 0.f, 0.f};
+    L.x0[tid] = t;
+  };
+  if (nj > 0) ld_ref(x);
+#endif
   for (int i = tid; i < 44 * 64; i += 512) {
     const c2 v = tov(a.xtab[i]);
     if (i < XT_R2) L.twr1[i >> 6][i & 63] = v;
@@ -165,7 +221,13 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   }
   const c2 csum = c2{a.cal_sum.x, a.cal_sum.y};
   const float invS = 1.0f / (float)S;
+#ifndef XK_NOREF
+  if (nj > 0) put_ref();
+#endif
   __syncthreads();
+#ifdef XK_PRIO     // A/B: static priority for the second-dispatched half of the waves (MI355X_MICROARCH item 4)
+  if (w >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #ifdef XK_STAMPS   // diagnostic build: per-phase time of block 0..255's steps (100 MHz clock)
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
   auto stamp = [&](int i) {
@@ -177,9 +239,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   auto stamp = [](int) {};
 #endif
 
-  using TP = std::conditional_t<H, h4v, f4v>;
-  const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
-  auto ld_chirp = [&](int64_t f, TP (&xin)[8]) {
+
+  auto ld_chirp = [&](int64_t f, TP (&xin)[8]) __attribute__((always_inline)) {
     const TP* __restrict__ q = iq + (f * C + (k * NW + w)) * (int64_t)S2;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -190,13 +251,22 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   };
 
   // ---------------- R: one chirp per wave (:203-205) ----------------
-  auto range = [&](const TP (&xin)[8], c2* __restrict__ slot) {
+#ifndef XK_NOREF
+  const bool refw = k == 0 && w == 0;                   // chirp 0: the frame's reference, transformed as it is
+  const float dsc = refw ? 0.f : 1.f;                   // other chirps: x - x_0 (cal cancels)
+  const c2 csum_w = refw ? csum : c2{0.f, 0.f};
+  const float calk = refw ? 1.f : 0.f;
+#endif
+  auto range = [&](const TP (&xin)[8], c2* __restrict__ slot) __attribute__((always_inline)) {
     c2 v[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       f4v t;
       if constexpr (H) t = __builtin_convertvector(xin[i], f4v);
       else t = xin[i];
+#ifndef XK_NOREF
+      t = __builtin_elementwise_fma(f4v{-dsc, -dsc, -dsc, -dsc}, L.x0[lane + 64 * i], t);   // x - x_0 (exact for near-equal values)
+#endif
       if constexpr (!FULL)
         if (!(lane + 64 * i < S2)) t = f4v{0.f, 0.f, 0.f, 0.f};
       v[2 * i] = t.xy;
@@ -205,12 +275,21 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     c2 sm = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
     for (int n = 4; n < 16; n += 4) sm += (v[n] + v[n + 1]) + (v[n + 2] + v[n + 3]);
+#ifndef XK_NOREF
+    const c2 mu = (wave_sum_c(sm) - csum_w) * invS;     // :204 mean of (x - cal), or of x - x_0, over the chirp
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      const f4v cp = L.cwp[n][lane];
+      v[n] = __builtin_elementwise_fma(v[n] - mu, cp.zz, -(cp.xy * calk));   // (x - cal - mu) w' / (d - mu_d) w'
+    }
+#else
     const c2 mu = (wave_sum_c(sm) - csum) * invS;       // :204 mean of (x - cal) over the chirp
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
       const f4v cp = L.cwp[n][lane];
       v[n] = __builtin_elementwise_fma(v[n] - mu, cp.zz, -cp.xy);   // (x - cal - mu) w'
     }
+#endif
     c2 z0[8], z1[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { z0[i] = v[2 * i]; z1[i] = v[2 * i + 1]; }
@@ -251,23 +330,42 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     dft8p(q1);
     // bins k1 + 16 hh + 8 e + 128 s2 -> group 4 s2 + 2 e + (k1 >> 2), position lane & 31
     const int c = k * NW + w;
-    c2* __restrict__ o = slot + (int64_t)((lane >> 5) * C + c) * GP + (lane & 31);
+    // slot stores are buffer stores (and the only ones in k_rdx): tools/check_vmcnt.py finds them
+    // by that to prove, on the built code, that every publish waits for them
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, NK * C * GP * 8, 0x00020000);
+#ifdef XK_SLOT16
+    {   // lane pairs swap one value: the even lane stores positions (p, p + 1) of group e = 0,
+        // the odd lane positions (p - 1, p) of group e = 1, one 16-byte store each
+      const bool odd = lane & 1;
+      const int o4 = (((lane >> 5) * C + c) * GP + (lane & 30) + (odd ? 2 * C * GP : 0)) * 8;
+#pragma unroll
+      for (int s2 = 0; s2 < 8; ++s2) {
+        const c2 snd = odd ? q0[s2] : q1[s2];
+        const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
+        const c2 lo = odd ? rcv : q0[s2], hi = odd ? q1[s2] : rcv;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, f4v{lo.x, lo.y, hi.x, hi.y}), rs,
+                                               o4 + 4 * s2 * C * GP * 8, 0, 0);
+      }
+    }
+#else
+    const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 8;
 #pragma unroll
     for (int s2 = 0; s2 < 8; ++s2) {
-      o[(int64_t)(4 * s2) * C * GP] = q0[s2];
-      o[(int64_t)(4 * s2 + 2) * C * GP] = q1[s2];
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q0[s2]), rs, o + 4 * s2 * C * GP * 8, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q1[s2]), rs, o + (4 * s2 + 2) * C * GP * 8, 0, 0);
     }
+#endif
   };
 
   // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259) ----------------
   // buffer_load ... sc1: the CU's L1 is bypassed (no stale lines from the slot's
   // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
-  auto ld_group = [&](const c2* __restrict__ grp, f4v (&t)[8]) {
+  auto ld_group = [&](const c2* __restrict__ grp, f4v (&t)[8]) __attribute__((always_inline)) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2*>(grp), (short)0, C * GP * 8, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
   };
-  auto stage = [&](const f4v (&t)[8]) {
+  auto stage = [&](const f4v (&t)[8]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int e4 = tid + 512 * i;
@@ -275,7 +373,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     }
   };
   // D of one frame from its staged group (the caller staged it and synchronised)
-  auto doppler_staged = [&](int64_t f) {
+  auto doppler_staged = [&](int64_t f) __attribute__((always_inline)) {
     const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
     const int r = xcd_bin(k, p);
     c2 xv[16];
@@ -284,6 +382,22 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) xv[i] = stg[(q + 16 * i) * 34 + p];
     }
+#ifndef XK_NOREF
+    // the slot holds X_0 for chirp 0 and X'_k = X_k - X_0 for the others (reference chirp above)
+    const c2 x0r = reinterpret_cast<const c2*>(L.u.stg)[p];   // X_0 of this row (chirp 0: q = 0, i = 0)
+    if (q == 0) xv[0] = c2{0.f, 0.f};                           // X'_0 = 0
+    // :210 / :265 row max |X| over the 256 chirps, X_k = X'_k + X_0
+    float pm = fmaxf(fmaxf(abs2v(xv[0] + x0r), abs2v(xv[1] + x0r)), fmaxf(abs2v(xv[2] + x0r), abs2v(xv[3] + x0r)));
+#pragma unroll
+    for (int i = 4; i < 16; i += 4)
+      pm = fmaxf(pm, fmaxf(fmaxf(abs2v(xv[i] + x0r), abs2v(xv[i + 1] + x0r)),
+                           fmaxf(abs2v(xv[i + 2] + x0r), abs2v(xv[i + 3] + x0r))));
+    // :217 row mean of the X'_k: X_k - mean(X) = X'_k - mean(X')
+    c2 sm = (xv[0] + xv[1]) + (xv[2] + xv[3]);
+#pragma unroll
+    for (int i = 4; i < 16; i += 4) sm += (xv[i] + xv[i + 1]) + (xv[i + 2] + xv[i + 3]);
+#else
+    const c2 x0r = c2{0.f, 0.f};
     // :217 row mean and :210 / :265 row max |X| over the 256 chirps
     c2 sm = (xv[0] + xv[1]) + (xv[2] + xv[3]);
     float pm = fmaxf(fmaxf(abs2v(xv[0]), abs2v(xv[1])), fmaxf(abs2v(xv[2]), abs2v(xv[3])));
@@ -292,12 +406,13 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       sm += (xv[i] + xv[i + 1]) + (xv[i + 2] + xv[i + 3]);
       pm = fmaxf(pm, fmaxf(fmaxf(abs2v(xv[i]), abs2v(xv[i + 1])), fmaxf(abs2v(xv[i + 2]), abs2v(xv[i + 3]))));
     }
+#endif
     sm = c2{row_sum16(sm.x), row_sum16(sm.y)};
     pm = __int_as_float(row_max16(__float_as_int(pm)));
     const c2 mu = sm * (1.0f / (float)C);
     const float pr = sqrtf(pm);
+    a.profile[f * NR + r] = pr;        // all 16 lanes of the row (same value): a store on every path
     if (q == 0) {
-      a.profile[f * NR + r] = pr;
       const double rng = (double)r * a.dist_per_bin;
       L.key[p] = (r >= 1 && r <= NR - 2 && rng >= a.min_d && rng <= a.max_d && pr > a.range_thr) ? pr : -1.f;
     }
@@ -316,7 +431,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
         if (sel >= 0 && r == sel) {
           float* __restrict__ row = a.cand_rows + ((f * XCD_TILES + k) * XCD_CAND + c) * (int64_t)C;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) row[q + 16 * i] = abs2v(xv[i]);
+          for (int i = 0; i < 16; ++i) row[q + 16 * i] = abs2v(xv[i] + x0r);
         }
         if (ki == sel) kv = -1.f;
       }
@@ -338,7 +453,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     dft16p<1>(xv);                     // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
     stamp(4);
     // :219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)]
-    if (a.rd) {
+    if constexpr (RD) {
       if constexpr (H) {
         __half2* __restrict__ out = reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + q;
 #pragma unroll
@@ -347,9 +462,29 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
           out[16 * d1s] = __floats2half2_rn(o.x, o.y);
         }
       } else {
+#ifdef XK_RD16
+        // lane pairs swap one value per pair of columns: 8 16-byte stores per lane
+        const bool odd = q & 1;
+        f4v* __restrict__ out4 = reinterpret_cast<f4v*>(reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + (q & 14));
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const c2 ve = xv[(2 * t + 8) & 15], vo = xv[(2 * t + 9) & 15];   // columns 2t, 2t + 1 (fftshift-ed)
+          const c2 snd = odd ? ve : vo;
+          const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
+          const c2 lo = odd ? rcv : ve, hi = odd ? vo : rcv;
+          // even lane: positions (q, q + 1) of column 2t; odd lane: (q - 1, q) of column 2t + 1
+          f4v* dst = out4 + (odd ? 16 * (2 * t + 1) / 2 : 16 * (2 * t) / 2);
+#ifdef XK_RD_WT
+          st_wt(dst, f4v{lo.x, lo.y, hi.x, hi.y});
+#else
+          __builtin_nontemporal_store(f4v{lo.x, lo.y, hi.x, hi.y}, dst);
+#endif
+        }
+#else
         f2v* __restrict__ out = reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + q;
 #pragma unroll
         for (int d1s = 0; d1s < 16; ++d1s) __builtin_nontemporal_store(xv[(d1s + 8) & 15], out + 16 * d1s);
+#endif
       }
     } else {   // :233 [val, di] = max(abs(.)) of the row: exact max of |D|^2, then its first position
       float m = abs2v(xv[8]);
@@ -361,33 +496,52 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       for (int d1s = 15; d1s >= 0; --d1s)
         if (abs2v(xv[(d1s + 8) & 15]) == rm) e = q + 16 * d1s;
       e = row_min16(e);
-      if (q == 0) a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);
+      a.rowpk[f * NR + r] = make_int2(__float_as_int(sqrtf(rm)), e);   // all lanes of the row: same value
     }
   };
 
   c2* __restrict__ slots0 = reinterpret_cast<c2*>(a.xcube) + (int64_t)x * NS * (NK * C * GP);
-  auto slot = [&](int j) { return slots0 + (int64_t)(j % NS) * (NK * C * GP); };
-  auto frame = [&](int j) { return x + 8 * (int64_t)j; };
+  auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % NS) * (NK * C * GP); };
+  auto frame = [&](int j) __attribute__((always_inline)) { return x + 8 * (int64_t)j; };
   // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - NS,
   // and R(j) runs after this member saw ready(j - 2); a member publishes R(j - 2)
   // only after its own reads of frame j - 4 (at most) have returned, so slots >= 4.
   TP xin[8];
   if (nj > 0) ld_chirp(frame(0), xin);
   // Step j: R(j - 1) is published first, its slot stores having drained under
-  // D(j - 3) (vmcnt counts the operations issued after them: the chirp loads, the
-  // profile store, the RD stores); then the group of frame j - 2 is loaded, R(j)
-  // runs while it lands, the group is staged once it is in (vmcnt(16): only R(j)'s
-  // slot stores behind it), the next chirp's loads go out and D(j - 2) runs.
-  // (first and last two steps peeled: in the steady loop the body is straight-line,
-  // so the compiler's own wait before the staging counts R(j)'s 16 slot stores)
-  auto body = [&](int j, bool dj, bool rj, bool pub) {
+  // D(j - 3): the wait counts the vector-memory operations every path issues
+  // after them (the next frame's reference and chirp loads, the profile store,
+  // the RD stores), which tools/check_vmcnt.py proves on the built code.  Then
+  // the group of frame j - 2 is loaded, R(j) runs while it lands, the group is
+  // staged once it is in (vmcnt(16): only R(j)'s slot stores behind it), the
+  // next chirp's loads go out and D(j - 2) runs.  Steps 0-2 and the last two
+  // are peeled and every flag is a compile-time constant, so each copy is
+  // straight-line code with a static wait count; the next frame's loads are
+  // unconditional (the last steady step reloads the last frame).
+  constexpr int kLd = 8 + (XK_REF ? 1 : 0);              // next frame's chirp (+ reference) loads
+  constexpr int kD = 1 + (RD ? XK_RD_STORES : 1);         // D's unconditional stores: profile + RD rows / row peaks
+  // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
+  auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto NEXT) __attribute__((always_inline)) {
+    const bool dj = DJ, rj = RJ, pub = PUB, next = NEXT;
     f4v grp[8];
     // one barrier for both: after it every wave's slot stores of R(j - 1) are in the
     // L2 (publish) and tid 0 has seen every member's R(j - 2) (the group may be read)
-    if (pub) vm_wait_le((j < nj ? 8 : 0) + (j - 1 >= 2 ? 1 + (a.rd ? 16 : 1) : 0));
-    if (dj && tid == 0) wait_ge(&ready[((j - 2) % NS) * 32], (unsigned)(NK * ((j - 2) / NS + 1)), a.xerr);
+    if (pub) vm_wait<decltype(CNT)::value>();
+    if (dj)   // wave 0 polls (scalar: its vector memory operations stay in flight); the barrier releases the rest
+      if (w == 0) wait_ge(&ready[((j - 2) % NS) * 32], (unsigned)(NK * ((j - 2) / NS + 1)), a.xctr + XCD_ABORT, a.xerr);
+#ifndef XK_NOREF
+    if (rj)
+      if (j >= 1) put_ref();           // frame j's reference chirp (R(j - 1) is done with the last one)
+#endif
     if (pub || dj) __syncthreads();
-    if (pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the publish: wave 0 adds 1 to the slot's ready counter; every other wave adds 0 to a word
+    // of its own, so that every wave issues the same vector-memory operations and the compiler's
+    // vmcnt waits behind them never wait for an atomic (a wave-0-only atomic made wave 0 wait
+    // for its return in R(j): the merged paths count it as possibly outstanding)
+    if (pub)
+      if (lane == 0)
+        __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % NS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
+                               w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dj) ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
     stamp(5);
     if (rj) range(xin, slot(j));
@@ -397,7 +551,13 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     __syncthreads();                   // the range transposes are free for the staging
     if (dj) stage(grp);
     cfence();
-    if (j + 1 < nj) ld_chirp(frame(j + 1), xin);   // in flight during D(j - 2)
+    if (next) {                        // in flight during D(j - 2)
+      const int jn = j + 1 < nj ? j + 1 : nj - 1;
+#ifndef XK_NOREF
+      ld_ref(frame(jn));
+#endif
+      ld_chirp(frame(jn), xin);
+    }
     stamp(1);
     if (dj) {
       __syncthreads();                 // staged
@@ -405,10 +565,21 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       doppler_staged(frame(j - 2));
     }
   };
-  int j = 0;
-  for (; j < 2 && j < nj + 2; ++j) body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj);
-  for (; j < nj; ++j) body(j, true, true, true);
-  for (; j < nj + 2; ++j) body(j, true, false, j - 1 < nj);
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  if (nj >= 3) {
+    body(0, F_{}, T_{}, F_{}, std::integral_constant<int, 0>{}, T_{});
+    body(1, F_{}, T_{}, T_{}, std::integral_constant<int, kLd>{}, T_{});
+    body(2, T_{}, T_{}, T_{}, std::integral_constant<int, kLd>{}, T_{});
+    for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, std::integral_constant<int, kLd + kD>{}, T_{});
+    body(nj, T_{}, F_{}, T_{}, std::integral_constant<int, kLd + kD>{}, F_{});
+    body(nj + 1, T_{}, F_{}, F_{}, std::integral_constant<int, 0>{}, F_{});
+  } else {
+    // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
+    // publish waiting for everything
+    for (int j = 0; j < nj + 2; ++j)
+      body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj, std::integral_constant<int, 0>{}, j + 1 < nj);
+  }
 #ifdef XK_STAMPS
   if (tid == 0) {
     for (int i = 0; i < 6; ++i) a.dbg[(int64_t)blockIdx.x * 8 + i] = st_acc[i];
@@ -431,9 +602,10 @@ __global__ __launch_bounds__(512, 1) void k_xcd_census(int* out) {
 // k_rdx needs all 256 of its workgroups resident together (team members wait for
 // each other), so two of its launches must never share a device at the same time:
 // launches from different streams (several contexts over one device, host threads)
-// are chained on the device through one event per device.  (Another process's
-// persistent kernel on the same GPU is not covered; the bounded waits then report
-// FMCW_E_HIP instead of hanging.)
+// are chained on the device through one event per device.  Only k_rdx launches are
+// chained: other kernels (RCCL's, another process's) run beside it; they finish on
+// their own, and while they hold CUs the bounded waits report FMCW_E_HIP (outputs
+// invalid) instead of hanging.
 namespace {
 std::mutex xcd_chain_mu;
 hipEvent_t xcd_chain_ev[64] = {};
@@ -449,17 +621,31 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   std::lock_guard<std::mutex> lk(xcd_chain_mu);
   if (!xcd_chain_ev[dev]) {
     if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
-  } else if ((e = hipStreamWaitEvent(s, xcd_chain_ev[dev], 0)) != hipSuccess) {
-    return e;
+  } else if (hipStreamWaitEvent(s, xcd_chain_ev[dev], 0) != hipSuccess) {
+    // a stale handle (the runtime tore the device's state down, e.g. hipDeviceReset): no
+    // earlier launch can still run, so a fresh event restarts the chain
+    (void)hipGetLastError();
+    if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
   }
   if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   const dim3 g(XCD_GRID), bl(64 * xk::NW);
+  const bool rd = a.rd != nullptr;
   if (a.S == op::NR) {
-    if (a.h) hipLaunchKernelGGL((k_rdx<true, true>), g, bl, 0, s, a);
-    else hipLaunchKernelGGL((k_rdx<true, false>), g, bl, 0, s, a);
+    if (a.h) {
+      if (rd) hipLaunchKernelGGL((k_rdx<true, true, true>), g, bl, 0, s, a);
+      else hipLaunchKernelGGL((k_rdx<true, true, false>), g, bl, 0, s, a);
+    } else {
+      if (rd) hipLaunchKernelGGL((k_rdx<true, false, true>), g, bl, 0, s, a);
+      else hipLaunchKernelGGL((k_rdx<true, false, false>), g, bl, 0, s, a);
+    }
   } else {
-    if (a.h) hipLaunchKernelGGL((k_rdx<false, true>), g, bl, 0, s, a);
-    else hipLaunchKernelGGL((k_rdx<false, false>), g, bl, 0, s, a);
+    if (a.h) {
+      if (rd) hipLaunchKernelGGL((k_rdx<false, true, true>), g, bl, 0, s, a);
+      else hipLaunchKernelGGL((k_rdx<false, true, false>), g, bl, 0, s, a);
+    } else {
+      if (rd) hipLaunchKernelGGL((k_rdx<false, false, true>), g, bl, 0, s, a);
+      else hipLaunchKernelGGL((k_rdx<false, false, false>), g, bl, 0, s, a);
+    }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   return hipEventRecord(xcd_chain_ev[dev], s);

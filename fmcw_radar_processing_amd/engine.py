@@ -44,8 +44,10 @@ class Engine:
     over them; include/fmcw.h fmcw_ctx_create).  No CPU fallback: raises if a
     device is absent."""
 
-    def __init__(self, device: int | list | tuple = 0):
+    def __init__(self, device: int | list | tuple | None = 0):
         self.lib = _lib.load()
+        if device is None:                       # FMCW_DEVICES, else every visible device
+            device = default_devices()
         ids = [int(device)] if isinstance(device, int) else [int(d) for d in device]
         arr = (ct.c_int32 * len(ids))(*ids)
         h = ct.c_void_p()
@@ -257,3 +259,12 @@ def device_count() -> int:
     n = ct.c_int32()
     st = lib.fmcw_device_count(ct.byref(n))
     return n.value if st == 0 else 0
+
+
+def default_devices() -> list:
+    """include/fmcw.h fmcw_default_devices: FMCW_DEVICES ("0,1,...") or every visible device."""
+    lib = _lib.load()
+    ids = (ct.c_int32 * 64)()
+    n = ct.c_int32()
+    check(lib.fmcw_default_devices(64, ids, ct.byref(n)))
+    return list(ids[: n.value])

@@ -12,7 +12,7 @@ import numpy as np
 from . import _lib
 
 _KIND = {np.dtype(np.float32): _lib.FMCW_JSON_F32, np.dtype(np.float64): _lib.FMCW_JSON_F64,
-         np.dtype(np.int32): _lib.FMCW_JSON_I32}
+         np.dtype(np.int32): _lib.FMCW_JSON_I32, np.dtype(np.uint8): _lib.FMCW_JSON_BOOL}
 
 
 def _field(name: str, v, keep: list) -> _lib.JsonField:
@@ -25,7 +25,9 @@ def _field(name: str, v, keep: list) -> _lib.JsonField:
         f.kind, f.data = _lib.FMCW_JSON_STRING, ct.cast(ct.c_char_p(b), ct.c_void_p)
         return f
     a = np.asarray(v)
-    if a.dtype == np.bool_ or np.issubdtype(a.dtype, np.integer):
+    if a.dtype == np.bool_:                  # MATLAB logical: true / false
+        a = a.astype(np.uint8)
+    elif np.issubdtype(a.dtype, np.integer):
         a = a.astype(np.int32) if a.size == 0 or (np.abs(a).max() < 2 ** 31) else a.astype(np.float64)
     elif a.dtype not in _KIND:
         a = a.astype(np.float64)

@@ -6,7 +6,7 @@ radar_processing.m writes every output through jsonencode (:315, :364, :392,
   * numeric 1x1 -> number; 1xN or Nx1 -> flat array; MxN (M, N > 1) -> array
     of M rows (row-major); 0x0 -> []
   * NaN, Inf, -Inf -> null
-  * char row -> string
+  * char row -> string; logical -> true / false (also inside arrays)
   * doubles are printed with up to 15 significant digits
 Consumers compare parsed numbers, not bytes.
 """
@@ -18,6 +18,8 @@ import numpy as np
 
 
 def _num(v) -> str:
+    if isinstance(v, (bool, np.bool_)):     # an element of a logical array
+        return "true" if v else "false"
     v = float(v)
     if math.isnan(v) or math.isinf(v):
         return "null"
@@ -62,7 +64,8 @@ def encode(obj, pretty: bool = True, ind: str = "") -> str:
         return "true" if obj else "false"
     if isinstance(obj, (int, float, np.integer, np.floating)):
         return _num(obj)
-    return _array(np.asarray(obj, dtype=np.float64), ind, pretty)
+    a = np.asarray(obj)
+    return _array(a if a.dtype == np.bool_ else a.astype(np.float64), ind, pretty)
 
 
 def matlab_squeeze_2d(a: np.ndarray) -> np.ndarray:

@@ -154,15 +154,18 @@ def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_
     frames = np.asarray(frames)
     F = frames.shape[0]
     own = engine is None
-    eng = Engine(0) if own else engine
+    eng = Engine(None) if own else engine                              # FMCW_DEVICES or every GPU
     try:
         eng.set_taps(cfg, cal)                                         # :138-139 windows
         flag = str(process_animal_activity).lower()
         if flag == "no":
-            return _run_no(eng, cfg, frames, F, filename, out_dir, upload)
-        if flag == "yes":
-            return _run_yes(eng, cfg, frames, F, filename, out_dir, upload)
-        return {"paths": []}                                            # :195/:440: neither branch
+            res = _run_no(eng, cfg, frames, F, filename, out_dir, upload)
+        elif flag == "yes":
+            res = _run_yes(eng, cfg, frames, F, filename, out_dir, upload)
+        else:
+            res = {"paths": []}                                         # :195/:440: neither branch
+        res["devices"] = list(eng.devices)                              # the GPUs this call drove
+        return res
     finally:
         if own:
             eng.close()

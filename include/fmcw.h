@@ -82,6 +82,15 @@ typedef struct fmcw_ctx fmcw_ctx;
 int32_t     fmcw_abi_version(void);
 const char* fmcw_last_error(void);
 int         fmcw_device_count(int32_t* n);
+/* The devices a caller that names none should use ("device choice
+ * comes from an env var or an explicit id"): the comma-separated ids of the
+ * environment variable FMCW_DEVICES (e.g. "0,1,2,3"), or every visible device
+ * when it is unset, empty or "all".  Writes up to cap ids to ids[], their count
+ * to *n.  FMCW_E_ARG for a malformed list or an id that is not present.  The
+ * MEX gateway's fmcw_mex('init') (no ids) and matlab/radar_processing.m use it,
+ * so one MATLAB call drives every GPU of the node (radar_processing_with_azure.m:50
+ * -> radar_processing.m:197). */
+int         fmcw_default_devices(int32_t cap, int32_t* ids, int32_t* n);
 
 /* Bind a context to n_devices HIP devices (device_ids[n_devices], or NULL for
  * 0 .. n_devices-1), each with its own streams, scratch and tables, all in the
@@ -311,12 +320,14 @@ int fmcw_render_spectrogram_device(fmcw_ctx* ctx, const float* d_Q, int32_t nq, 
  *   FMCW_JSON_F32/F64/I32  a rows x cols MATLAB array; element (i, j) at
  *     data[i * row_stride + j * col_stride] (so a [nseg][nbins] device-layout
  *     intensity is written as MATLAB's nbins x nseg without a transpose).
+ *   FMCW_JSON_BOOL    the same with uint8 elements (0 / non-0): a MATLAB logical
+ *     array, written as true / false.
  * jsonencode's shape rules: 1x1 -> number, 1xN / Nx1 -> flat array, MxN ->
  * array of M rows, empty -> []; NaN/Inf -> null; numbers as "%.15g" (integers
  * without a fraction).  threads <= 0: up to 16 host threads format in parallel.
  * No device work; no context needed.
  * ------------------------------------------------------------------------- */
-enum { FMCW_JSON_STRING = 0, FMCW_JSON_F32 = 1, FMCW_JSON_F64 = 2, FMCW_JSON_I32 = 3 };
+enum { FMCW_JSON_STRING = 0, FMCW_JSON_F32 = 1, FMCW_JSON_F64 = 2, FMCW_JSON_I32 = 3, FMCW_JSON_BOOL = 4 };
 typedef struct {
   const char* name;
   int32_t kind;

@@ -43,7 +43,9 @@ P = struct('nts', nts, 'pn', pn, 'nr', nr, 'nd', nd, 'max_targets', 1, ...
 n_cal = length(calib_data) / (2 * n_rx);
 step = n_cal / nts;
 cal = complex(calib_data(1:step:n_cal), calib_data(n_cal+1:step:2*n_cal)).';
-fmcw_mex('init', 0);
+fmcw_mex('init');                        % FMCW_DEVICES (e.g. '0,1,2,3'), else every visible GPU
+used_devices = fmcw_mex('devices');
+fprintf('radar_processing: DSP on %d GPU(s): %s\n', numel(used_devices), mat2str(used_devices));
 fmcw_mex('taps', P, single(2 * blackman(nts)), single(2 * chebwin(pn)), single(complex(cal)));
 
 % ---- the loop on the GPU (reference :197-261) ----------------------------------

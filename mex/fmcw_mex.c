@@ -5,9 +5,12 @@
  * radar_processing(process_animal_activity) of the reference
  * (radar-etl-pipeline/radar_processing.m:56) and calls:
  *
- *   fmcw_mex('init', device_ids)                                 -> fmcw_ctx_create (once; mexLock);
- *                                        device_ids: vector, default 0; several ids = one context over
- *                                        several GPUs (frames and STFT segments sharded, RCCL max)
+ *   fmcw_mex('init' [, device_ids])                              -> fmcw_ctx_create (once; mexLock);
+ *                                        device_ids: vector; without it fmcw_default_devices (the env
+ *                                        var FMCW_DEVICES, else every visible GPU); several ids = one
+ *                                        context over several GPUs (frames and STFT segments sharded,
+ *                                        RCCL max)
+ *   ids = fmcw_mex('devices')                                    -> fmcw_ctx_devices (the ids in use)
  *   fmcw_mex('taps', P, range_win, doppler_win, calib_rx1)       -> fmcw_set_taps       (:138-139, :174)
  *   [prof, cnt, ridx, rmag, didx, slow, probe] =
  *       fmcw_mex('process', P, iq, probe_column)                  -> fmcw_process        (:197-261, :265, :410)
@@ -98,7 +101,9 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
     if (!g_ctx) {
       int32_t ids[64] = {0};
       int32_t n = 1;
-      if (nrhs > 1) {
+      if (nrhs < 2) {
+        check(fmcw_default_devices(64, ids, &n));
+      } else {
         const mxArray* a = prhs[1];
         if (!mxIsDouble(a) || mxIsComplex(a) || mxGetNumberOfElements(a) < 1 || mxGetNumberOfElements(a) > 64)
           mexErrMsgIdAndTxt("fmcw:arg", "init: device_ids must be a real double vector of 1..64 ids");
@@ -109,6 +114,14 @@ void mexFunction(int nlhs, mxArray* plhs[], int nrhs, const mxArray* prhs[]) {
       mexLock();
       mexAtExit(at_exit);
     }
+    return;
+  }
+  if (!strcmp(cmd, "devices")) {            /* ids = fmcw_mex('devices'): the context's device ids */
+    if (!g_ctx) mexErrMsgIdAndTxt("fmcw:state", "call fmcw_mex('init') first");
+    int32_t ids[64], n = 0, rc = 0;
+    check(fmcw_ctx_devices(g_ctx, &n, ids, &rc));
+    plhs[0] = mxCreateDoubleMatrix(1, n, mxREAL);
+    for (int32_t i = 0; i < n; ++i) mxGetDoubles(plhs[0])[i] = ids[i];
     return;
   }
   if (!strcmp(cmd, "close")) {

@@ -32,6 +32,7 @@ int32_t* mxGetInt32s(const mxArray* a);
 mxComplexSingle* mxGetComplexSingles(const mxArray* a);
 mxArray* mxCreateNumericMatrix(mwSize m, mwSize n, mxClassID c, mxComplexity x);
 mxArray* mxCreateDoubleScalar(double v);
+mxArray* mxCreateDoubleMatrix(mwSize m, mwSize n, mxComplexity x);
 int mxIsChar(const mxArray* a);
 int mxIsInt32(const mxArray* a);
 int mxGetNumberOfFields(const mxArray* s);

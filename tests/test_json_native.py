@@ -34,6 +34,18 @@ def test_shapes_and_values(tmp_path, pretty):
     _same(tmp_path, obj, pretty)
 
 
+@pytest.mark.parametrize("pretty", [True, False])
+def test_logicals(tmp_path, pretty):
+    """MATLAB logicals encode as true / false, scalars and arrays alike (jsonencode)."""
+    obj = {"flag": True, "off": np.bool_(False), "mask": np.array([True, False, True]),
+           "grid": np.array([[True, False], [False, False], [True, True]]), "col": np.array([[False], [True]])}
+    got = _same(tmp_path, obj, pretty)
+    import json
+    d = json.loads(got)
+    assert d["flag"] is True and d["off"] is False and d["mask"] == [True, False, True]
+    assert d["grid"] == [[True, False], [False, False], [True, True]] and d["col"] == [False, True]
+
+
 @pytest.mark.parametrize("threads", [1, 3, 0])
 def test_large_arrays_cross_pieces(tmp_path, threads):
     """Vectors and matrices larger than one formatting piece (65536 elements)."""
