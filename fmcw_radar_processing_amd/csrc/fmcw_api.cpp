@@ -401,34 +401,40 @@ int fmcw_device_count(int32_t* n) {
 int fmcw_default_devices(int32_t cap, int32_t* ids, int32_t* n) {
   if (!ids || !n || cap < 1) return fail(FMCW_E_ARG, "ids/n NULL or cap < 1");
   *n = 0;
-  int nd = 0;
-  hipError_t e = hipGetDeviceCount(&nd);
-  if (e != hipSuccess) return fail(FMCW_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
   const char* env = std::getenv("FMCW_DEVICES");
   std::string v = env ? env : "";
   v.erase(std::remove_if(v.begin(), v.end(), [](char ch) { return ch == ' ' || ch == '\t'; }), v.end());
-  if (v.empty() || v == "all") {
+  std::vector<long> want;                      // the list is parsed before any device is asked about
+  if (!v.empty() && v != "all") {
+    size_t pos = 0;
+    while (pos <= v.size()) {
+      const size_t end = std::min(v.find(',', pos), v.size());
+      const std::string tok = v.substr(pos, end - pos);
+      char* stop = nullptr;
+      const long id = tok.empty() ? -1 : std::strtol(tok.c_str(), &stop, 10);
+      if (tok.empty() || *stop != '\0' || id < 0) return fail(FMCW_E_ARG, "FMCW_DEVICES: malformed list '" + v + "'");
+      want.push_back(id);
+      pos = end + 1;
+    }
+    if ((int64_t)want.size() > cap) return fail(FMCW_E_ARG, "FMCW_DEVICES: more ids than cap");
+  }
+  int nd = 0;
+  hipError_t e = hipGetDeviceCount(&nd);
+  if (e != hipSuccess) return fail(FMCW_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  if (want.empty()) {
     if (nd < 1) return fail(FMCW_E_HIP, "no HIP device present");
     const int m = std::min<int>(nd, cap);
     for (int i = 0; i < m; ++i) ids[i] = i;
     *n = m;
     return FMCW_OK;
   }
-  int32_t m = 0;
-  size_t pos = 0;
-  while (pos <= v.size()) {
-    const size_t end = std::min(v.find(',', pos), v.size());
-    const std::string tok = v.substr(pos, end - pos);
-    char* stop = nullptr;
-    const long id = tok.empty() ? -1 : std::strtol(tok.c_str(), &stop, 10);
-    if (tok.empty() || *stop != '\0') return fail(FMCW_E_ARG, "FMCW_DEVICES: malformed list '" + v + "'");
-    if (id < 0 || id >= nd)
-      return fail(FMCW_E_ARG, "FMCW_DEVICES: device " + tok + " not present (" + std::to_string(nd) + " devices)");
-    if (m >= cap) return fail(FMCW_E_ARG, "FMCW_DEVICES: more ids than cap");
-    ids[m++] = (int32_t)id;
-    pos = end + 1;
+  for (size_t i = 0; i < want.size(); ++i) {
+    if (want[i] >= nd)
+      return fail(FMCW_E_ARG, "FMCW_DEVICES: device " + std::to_string(want[i]) + " not present (" +
+                                  std::to_string(nd) + " devices)");
+    ids[i] = (int32_t)want[i];
   }
-  *n = m;
+  *n = (int32_t)want.size();
   return FMCW_OK;
 }
 

@@ -85,6 +85,30 @@ def test_no_cpu_fallback_without_a_device():
         Engine([0, 1])
 
 
+@pytest.mark.parametrize("spec", ["0,x", "1,,2", "-1", "a"])
+def test_default_devices_rejects_a_malformed_list(monkeypatch, spec):
+    """FMCW_DEVICES (fmcw_default_devices, the MEX drop-in's device choice) is parsed before
+    any device is asked about: a malformed list is an argument error on any host."""
+    monkeypatch.setenv("FMCW_DEVICES", spec)
+    lib = _lib.load()
+    ids = (ct.c_int32 * 8)()
+    n = ct.c_int32(-1)
+    assert lib.fmcw_default_devices(8, ids, ct.byref(n)) == _lib.FMCW_E_ARG
+    assert n.value == 0 and "FMCW_DEVICES" in lib.fmcw_last_error().decode()
+    assert lib.fmcw_default_devices(0, ids, ct.byref(n)) == _lib.FMCW_E_ARG
+
+
+def test_default_devices_without_a_device(monkeypatch):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    monkeypatch.delenv("FMCW_DEVICES", raising=False)
+    lib = _lib.load()
+    ids = (ct.c_int32 * 8)()
+    n = ct.c_int32()
+    assert lib.fmcw_default_devices(8, ids, ct.byref(n)) == _lib.FMCW_E_HIP
+
+
 def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "_lib", None)
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))

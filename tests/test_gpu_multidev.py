@@ -112,3 +112,31 @@ def test_rccl_context_over_distinct_devices(engine):
     for k in ref:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     np.testing.assert_array_equal(sgot["intensity"], sref["intensity"])
+
+
+def test_default_devices_drive_every_gpu(engine, monkeypatch):
+    """fmcw_default_devices (the drop-in's choice: matlab/radar_processing.m fmcw_mex('init'),
+    radar.radar_processing with no engine): every visible GPU unless FMCW_DEVICES names some;
+    a context over them gives the one-device results."""
+    from fmcw_radar_processing_amd.engine import default_devices
+    monkeypatch.delenv("FMCW_DEVICES", raising=False)
+    assert default_devices() == list(range(_n_gpus()))
+    monkeypatch.setenv("FMCW_DEVICES", "0,0")
+    assert default_devices() == [0, 0]
+    monkeypatch.setenv("FMCW_DEVICES", str(_n_gpus()))
+    from fmcw_radar_processing_amd import FmcwError
+    with pytest.raises(FmcwError, match="E_ARG"):
+        default_devices()
+    monkeypatch.setenv("FMCW_DEVICES", "0,0")
+    cfg, p, wr, wd, cal, iq = _frames(5, GEOMS[1], frame0=3)
+    engine.set_taps(cfg, cal, wr, wd)
+    ref = engine.process(iq)
+    multi = Engine(None)
+    try:
+        assert multi.devices == [0, 0]
+        multi.set_taps(cfg, cal, wr, wd)
+        got = multi.process(iq)
+    finally:
+        multi.close()
+    for k in ref:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
