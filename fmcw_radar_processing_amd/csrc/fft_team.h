@@ -6,8 +6,8 @@
 // by one radix-2/4/8 pass (N = 16^a * R0), e.g. 1024 = 16*16*4, 256 = 16*16.
 // Inside a pass every thread does its butterflies entirely in registers; the
 // data exchange between passes goes through the team's LDS region, padded by
-// one complex every 16 so the stride-16 write of pass 1 is bank-conflict free
-// (ds_write_b64: 16-lane groups, bank = dword mod 32).
+// one complex every 16 (32 for N >= 512) so the stride-16 write of pass 1 and
+// the reads are bank-conflict free (FftPlan::PADSH).
 //
 // Data distribution (the property the kernels are built on):
 //   on entry  thread t holds x[t + T*m], m = 0..P-1  ("cyclic")
@@ -145,13 +145,19 @@ template <int N> struct FftPlan {
   static_assert(N >= 2 && N <= 4096 && (N & (N - 1)) == 0, "FFT size must be a power of two");
   static constexpr int P = N < 16 ? N : 16;   // values per thread
   static constexpr int T = N / P;             // threads per team
-  static constexpr int LDS = (N < 16) ? 0 : N + N / 16;  // complex elements of LDS per team
+  // LDS padding: one complex every 2^PADSH.  Teams of >= 32 threads (N >= 512) pad one in
+  // 32: the first pass's stores (lane t writes 16 t + r, 16-lane ds_write_b64 groups) and
+  // every pass's loads (32 consecutive elements per 32-lane ds_read_b64 group) are then
+  // conflict-free (a 1-in-16 pad maps elements 0 and 31 of a load onto one bank pair).
+  // Smaller teams share 32-lane groups and keep the 1-in-16 pad with odd team strides.
+  static constexpr int PADSH = T >= 32 ? 5 : 4;
+  static constexpr int LDS = (N < 16) ? 0 : N + (N >> PADSH);  // complex elements of LDS per team
   // stride between the LDS regions of teams that share a wave: odd, so the same
   // element of 16 neighbouring teams lands on 16 different bank pairs
   static constexpr int STRIDE = (N < 16) ? 0 : (LDS | 1);
 };
 
-__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
+template <int N> __device__ __forceinline__ int lds_pad(int i) { return i + (i >> FftPlan<N>::PADSH); }
 
 constexpr int fft_num_r16(int n) { return n >= 16 ? 1 + fft_num_r16(n / 16) : 0; }
 constexpr int fft_pow16(int k) { return k == 0 ? 1 : 16 * fft_pow16(k - 1); }
@@ -259,6 +265,11 @@ __device__ __forceinline__ void stockham_pass_regs(float2* v, int t, const TW& s
 }
 
 // Write the pass output to LDS: out[(j/Ns)*Ns*R + j%Ns + r*Ns] = v[q*R + r].
+// One 8-byte store per element (ds_write_b64, 16-lane groups): the 1-in-16 pad
+// makes the stride-16 first pass conflict-free for exactly that width, so the
+// compiler must not merge a lane's adjacent elements into write2 / b128 forms
+// (2-way conflicts: b32 halves in 32-lane groups, b128 spans of 4 banks) -- the
+// empty asm between the stores keeps them separate.
 template <int N, int R, int Ns>
 __device__ __forceinline__ void stockham_store_lds(const float2* v, int t, float2* lds) {
   constexpr int P = FftPlan<N>::P, T = FftPlan<N>::T, Q = P / R;
@@ -267,7 +278,10 @@ __device__ __forceinline__ void stockham_store_lds(const float2* v, int t, float
     const int j = t + T * q;
     const int base = (j / Ns) * Ns * R + (j & (Ns - 1));
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[lds_pad(base + r * Ns)] = v[q * R + r];
+    for (int r = 0; r < R; ++r) {
+      *reinterpret_cast<double*>(&lds[lds_pad<N>(base + r * Ns)]) = __builtin_bit_cast(double, v[q * R + r]);
+      asm volatile("" ::: "memory");
+    }
   }
 }
 
@@ -278,7 +292,7 @@ __device__ __forceinline__ void stockham_load_lds(float2* v, int t, const float2
 #pragma unroll
   for (int q = 0; q < Q; ++q)
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[q * R + r] = lds[lds_pad(t + T * q + r * (N / R))];
+    for (int r = 0; r < R; ++r) v[q * R + r] = lds[lds_pad<N>(t + T * q + r * (N / R))];
 }
 
 // Recursive pass driver.  `PASS` indexes the pass, Ns = product of radices so far.

@@ -12,6 +12,7 @@
 // served by the XCD's L2 (MI355X_MICROARCH.md, visibility table).  The
 // stand-alone kernels read data written by an earlier launch and use plain loads.
 #pragma once
+#include <type_traits>
 #include <climits>
 
 #include "fft_team.h"
@@ -43,15 +44,35 @@ template <bool NT> __device__ __forceinline__ float ldf(const float* p, int64_t 
   else return p[i];
 }
 
+// Sum over aligned groups of W lanes (W = 2..64) by DPP and the half-wave swaps -- no
+// LDS (a __shfl_xor is a ds_bpermute through the LDS crossbar).  xor 1, xor 2, then
+// the row mirrors on group-uniform values (xor 4, xor 8), then the 16- and 32-lane
+// swaps; symmetric pairings, so every lane of a group gets the same bits.
+template <int W> __device__ __forceinline__ float group_sum(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xF, 0xF, true));
+  };
+  if constexpr (W >= 2) v += dpp(v, std::integral_constant<int, 0xB1>{});    // quad_perm [1,0,3,2]
+  if constexpr (W >= 4) v += dpp(v, std::integral_constant<int, 0x4E>{});    // quad_perm [2,3,0,1]
+  if constexpr (W >= 8) v += dpp(v, std::integral_constant<int, 0x141>{});   // row_half_mirror
+  if constexpr (W >= 16) v += dpp(v, std::integral_constant<int, 0x140>{});  // row_mirror
+  if constexpr (W >= 32) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  if constexpr (W >= 64) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  return v;
+}
+
 // team-wide sum of a complex value over T threads that are consecutive lanes
 template <int T>
 __device__ __forceinline__ float2 team_sum(float2 s, float2* red, int t) {
   constexpr int W = T < 64 ? T : 64;
-#pragma unroll
-  for (int o = W / 2; o > 0; o >>= 1) {
-    s.x += __shfl_xor(s.x, o);
-    s.y += __shfl_xor(s.y, o);
-  }
+  s.x = group_sum<W>(s.x);
+  s.y = group_sum<W>(s.y);
   if constexpr (T > 64) {
     // teams span T/64 waves (T = 128 for Nr = 2048): combine through LDS
     if ((t & 63) == 0) red[t >> 6] = s;

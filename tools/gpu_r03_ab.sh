@@ -14,10 +14,23 @@ for n in ${TESTS:-$names}; do
   echo "$n tests rc=$rc: $(tail -1 gpurun_out/abt_$n.log)"
   [ $rc -ne 0 ] && { tail -30 gpurun_out/abt_$n.log; exit $rc; }
 done
+for n in ${FULLTEST:-}; do
+  FMCW_LIB=ab/$n.so timeout -k 10 600 python -u -m pytest tests -m gpu -q -x --timeout 120 \
+    --timeout-method thread > gpurun_out/abft_$n.log 2>&1; rc=$?
+  echo "$n full gpu tests rc=$rc: $(tail -1 gpurun_out/abft_$n.log)"
+  [ $rc -ne 0 ] && { tail -30 gpurun_out/abft_$n.log; exit $rc; }
+done
 for i in $(seq $N); do
   for n in $names; do
     echo -n "$n: "
     FMCW_LIB=ab/$n.so timeout -k 10 120 python -u tools/onepass_perf.py 4096 20 xcd > gpurun_out/ab_$n.log 2>&1 || { tail -5 gpurun_out/ab_$n.log; exit 1; }
     grep -E "^xcd| onepass |xk-stamps" gpurun_out/ab_$n.log | tr -s ' ' | tr '\n' ' '; echo
+  done
+done
+for i in $(seq $N); do
+  for n in ${K1:-}; do
+    echo -n "$n: "
+    FMCW_LIB=ab/$n.so timeout -k 10 120 python -u tools/k1_perf.py > gpurun_out/k1_$n.log 2>&1 || { tail -5 gpurun_out/k1_$n.log; exit 1; }
+    grep "^k1" gpurun_out/k1_$n.log
   done
 done
