@@ -166,7 +166,7 @@ void shard(int64_t total, int g, int world, int64_t& f0, int64_t& n) {
   n = base + (g < rem ? 1 : 0);
 }
 
-constexpr int kStages = 10;  // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call, 8 k_rd1p, 9 render
+constexpr int kStages = 10;  // 0..6 per kernel (see fmcw.h), 7 range+Doppler span per call, 8 k_rdx, 9 render
 
 }  // namespace
 
@@ -222,11 +222,11 @@ struct fmcw_ctx {
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
-  DevBuf op_gh, op_tab;                        // single-pass tables (fmcw::OP_TAB_*)
   DevBuf x_cube, x_ctr, x_err, x_tab;          // XCD-team schedule: hand-off slots, counters, sticky error, XT_* table
-  int xcd_ok = -1;                             // census of the device (-1 not run yet)
+  int xcd_teams = -1;                          // census of the device: its XCD teams (-1 not run yet, 0 none)
+  int8_t xcc_team[16] = {};                    // HW_REG_XCC_ID -> team
   bool xcd_used = false;                       // a k_rdx launch since the last error check
-  float op_gh_scale = 0.f;                     // IF_scale op_gh was built for (0 = stale)
+  bool x_tab_ok = false;                       // x_tab built for the current taps
   // Multi-device context (fmcw_ctx_create with n_devices > 1): this object is
   // device 0 of the context and peers[i] a full context on device i + 1.  The
   // host-pointer calls shard their frames (fmcw_process, fmcw_range_fft) or
@@ -548,7 +548,7 @@ int fmcw_set_taps(fmcw_ctx* c, const fmcw_params* p, const float* range_win, con
   CHK(upload_twiddles(c->tw_nd, p->nd, s));
   c->p = *p;
   c->taps = true;
-  c->op_gh_scale = 0.f;
+  c->x_tab_ok = false;
   for (fmcw_ctx* q : c->peers) CHK(fmcw_set_taps(q, p, range_win, doppler_win, calib));
   return FMCW_OK;
 }
@@ -632,116 +632,46 @@ int fmcw_timing_reset(fmcw_ctx* c) {
 // ---------------------------------------------------------------------------
 // per-frame stages
 // ---------------------------------------------------------------------------
-// Per-bin linearity constants of the single-pass range stage (kernels_onepass.hip):
-// Gh[r] = DFT((cal - mean(cal)) w')[r], Hh[r] = DFT(w')[r], w' = float(IF_scale w)
-// (the values K1 uses), accumulated in float64 and rounded once.
-static int build_onepass_gh(fmcw_ctx* c, float if_scale, hipStream_t s) {
-  const int S = c->p.nts, NR = c->p.nr, n = std::min(S, NR);
+// Twiddle table of the XCD-team schedule (kernels_xcd.hip, XT_* sections, lane order [..][64]),
+// built in float64 and rounded once; it depends only on NR, so it is built once per context.
+static int build_xcd_tab(fmcw_ctx* c, hipStream_t s) {
+  const int NR = c->p.nr;
   std::vector<double> cr(NR), ci(NR);
   for (int i = 0; i < NR; ++i) {
     const double a = -2.0 * M_PI * (double)i / (double)NR;
     cr[i] = std::cos(a);
     ci[i] = std::sin(a);
   }
-  double mr = 0, mi = 0;
-  for (int i = 0; i < S; ++i) { mr += c->h_cal[2 * i]; mi += c->h_cal[2 * i + 1]; }
-  mr /= S;
-  mi /= S;
-  std::vector<double> wf(n), gr(n), gi(n);
-  for (int i = 0; i < n; ++i) {
-    wf[i] = (double)(float)((double)if_scale * c->h_wr[i]);
-    gr[i] = ((double)c->h_cal[2 * i] - mr) * wf[i];
-    gi[i] = ((double)c->h_cal[2 * i + 1] - mi) * wf[i];
-  }
-  std::vector<float> t(4 * (size_t)NR), g(4 * (size_t)NR);
-  for (int r = 0; r < NR; ++r) {
-    double Gr = 0, Gi = 0, Hr = 0, Hi = 0;
-    for (int i = 0, idx = 0; i < n; ++i, idx = (idx + r) & (NR - 1)) {
-      Gr += gr[i] * cr[idx] - gi[i] * ci[idx];
-      Gi += gr[i] * ci[idx] + gi[i] * cr[idx];
-      Hr += wf[i] * cr[idx];
-      Hi += wf[i] * ci[idx];
-    }
-    t[4 * r] = (float)Gr; t[4 * r + 1] = (float)Gi; t[4 * r + 2] = (float)Hr; t[4 * r + 3] = (float)Hi;
-  }
-  // lane order of k_rd1p: [tile t][slot s][lane l] holds bin t + 8 (lane_bin(l) + 64 s),
-  // lane_bin(l) = 4 bitrev4(l mod 16) + l / 16 (kernels_onepass.hip)
-  auto lane_bin = [](int l) { int r = 0; for (int i = 0; i < 4; ++i) r |= ((l >> i) & 1) << (5 - i); return r + (l >> 4); };
-  for (int tt = 0; tt < fmcw::OP_TILES; ++tt)
-    for (int sl = 0; sl < 2; ++sl)
-      for (int l = 0; l < 64; ++l) {
-        const int r = tt + 8 * (lane_bin(l) + 64 * sl), o = ((tt * 2 + sl) * 64 + l) * 4;
-        for (int q = 0; q < 4; ++q) g[o + q] = t[4 * r + q];
-      }
-  std::vector<float> tab(2 * (size_t)fmcw::OP_TAB_SIZE);
-  auto put = [&](int idx, double re, double im) { tab[2 * idx] = (float)re; tab[2 * idx + 1] = (float)im; };
+  std::vector<float> xt(2 * (size_t)fmcw::XT_SIZE);
+  auto xput = [&](int idx, int e1024) { xt[2 * idx] = (float)cr[e1024 & (NR - 1)]; xt[2 * idx + 1] = (float)ci[e1024 & (NR - 1)]; };
   for (int l = 0; l < 64; ++l) {
-    for (int i = 0; i < 5; ++i) {            // span hh = 32 >> i: W_{2 hh}^(l mod hh), on every lane for the
-      const int hh = 32 >> i;                // pair butterflies (spans 32, 16), on set lanes for spans 8, 4, 2
-      const int e = (hh >= 16 || (l & hh)) ? ((l & (hh - 1)) * (512 / hh)) & (NR - 1) : 0;
-      put(fmcw::OP_TAB_LANE + i * 64 + l, cr[e], ci[e]);
-    }
-    const int e = 8 * lane_bin(l);
-    put(fmcw::OP_TAB_LANE + 5 * 64 + l, cr[e], ci[e]);
+    for (int k1 = 1; k1 < 8; ++k1)
+      for (int e = 0; e < 2; ++e) xput(fmcw::XT_R1 + (2 * (k1 - 1) + e) * 64 + l, (2 * l + e) * k1);   // W1024^(a k1)
+    for (int s1 = 1; s1 < 16; ++s1) xput(fmcw::XT_R2 + (s1 - 1) * 64 + l, 8 * ((l & 7) * s1));      // W128^(a0 s1)
+    for (int d0 = 1; d0 < 16; ++d0) xput(fmcw::XT_D1 + (d0 - 1) * 64 + l, 4 * ((l & 15) * d0));     // W256^(q d0)
   }
-  for (int i = 0; i < 8; ++i)
-    for (int d = 0; d < 32; ++d) {
-      const double a = -2.0 * M_PI * (double)((i * d) & 255) / 256.0;
-      put(fmcw::OP_TAB_TWR + i * 32 + d, std::cos(a), std::sin(a));
-    }
-  for (int e = 0; e < 256; ++e)               // W256^(e d2) = W1024^(4 e d2)
-    for (int d = 0; d < 32; ++d) put(fmcw::OP_TAB_TWR2 + e * 32 + d, cr[(4 * e * d) & (NR - 1)], ci[(4 * e * d) & (NR - 1)]);
-  for (int tt = 0; tt < 8; ++tt)
-    for (int j = 0; j < 8; ++j)
-      for (int e = 0; e < 2; ++e)
-        for (int l = 0; l < 64; ++l) {
-          const int nn = 2 * l + e + 128 * j, idx = (tt * nn) & (NR - 1);
-          const double wv = nn < n ? wf[nn] : 0.0;
-          put(fmcw::OP_TAB_CST + ((tt * 8 + j) * 2 + e) * 64 + l, (double)(float)cr[idx] * wv,
-              (double)(float)ci[idx] * wv);
-        }
-  {   // XCD-team schedule twiddles (kernels_xcd.hip), lane order [..][64]
-    std::vector<float> xt(2 * (size_t)fmcw::XT_SIZE);
-    auto xput = [&](int idx, int e1024) { xt[2 * idx] = (float)cr[e1024 & (NR - 1)]; xt[2 * idx + 1] = (float)ci[e1024 & (NR - 1)]; };
-    for (int l = 0; l < 64; ++l) {
-      for (int k1 = 1; k1 < 8; ++k1)
-        for (int e = 0; e < 2; ++e) xput(fmcw::XT_R1 + (2 * (k1 - 1) + e) * 64 + l, (2 * l + e) * k1);   // W1024^(a k1)
-      for (int s1 = 1; s1 < 16; ++s1) xput(fmcw::XT_R2 + (s1 - 1) * 64 + l, 8 * ((l & 7) * s1));      // W128^(a0 s1)
-      for (int d0 = 1; d0 < 16; ++d0) xput(fmcw::XT_D1 + (d0 - 1) * 64 + l, 4 * ((l & 15) * d0));     // W256^(q d0)
-    }
-    CHK(c->x_tab.ensure(xt.size() * 4));
-    HIPCHK(hipMemcpyAsync(c->x_tab.p, xt.data(), xt.size() * 4, hipMemcpyHostToDevice, s));
-  }
-  CHK(c->op_gh.ensure(g.size() * 4));
-  HIPCHK(hipMemcpyAsync(c->op_gh.p, g.data(), g.size() * 4, hipMemcpyHostToDevice, s));
-  CHK(c->op_tab.ensure(tab.size() * 4));
-  HIPCHK(hipMemcpyAsync(c->op_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice, s));
+  CHK(c->x_tab.ensure(xt.size() * 4));
+  HIPCHK(hipMemcpyAsync(c->x_tab.p, xt.data(), xt.size() * 4, hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
-  c->op_gh_scale = if_scale;
+  c->x_tab_ok = true;
   return FMCW_OK;
 }
 
-// Single-pass schedule (kernels_onepass.hip): k_rd1p computes range FFT,
-// profile, Doppler FFT and the per-row Doppler peaks of each frame without a
-// range cube; k_detect_1p runs the detection; k_slow_fix recomputes the rare
-// slow-time row that was not among a tile's candidates.  Chunks bound the
-// candidate scratch (OP_TILES*OP_CAND rows of PN floats per frame).
-// Hand-off slots per XCD of the XCD-team schedule (4; FMCW_XCD_SLOTS may ask for more, up to XCD_MAX_SLOTS).
-static int xcd_slots() {
-  const char* e = std::getenv("FMCW_XCD_SLOTS");
-  const int v = e ? std::atoi(e) : 4;
-  return std::min(std::max(v, 4), fmcw::XCD_MAX_SLOTS);
-}
-
+// Single-pass schedule (kernels_xcd.hip): k_rdx computes range FFT, profile,
+// Doppler FFT and the slow-time candidate rows of each frame, the range cube
+// handed between the CUs of one XCD; k_detect_1p runs the detection; k_slow_fix
+// recomputes the rare slow-time row that was not among a group's candidates.
+// Chunks bound the candidate scratch (XCD_TILES * XCD_CAND rows of PN floats per
+// frame).  The hand-off ring has XCD_MAX_SLOTS slots per XCD.
 static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int h, int64_t F, float* d_prof,
                            int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
-                           void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s, bool xcd) {
+                           void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
   const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
   const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : 8192);
-  const int tiles = xcd ? fmcw::XCD_TILES : fmcw::OP_TILES, ncand = xcd ? fmcw::XCD_CAND : fmcw::OP_CAND;
+  const int tiles = fmcw::XCD_TILES, ncand = fmcw::XCD_CAND;
   const int TC = tiles * ncand;
-  const int slots = xcd_slots();
-  if (xcd) {
+  const int slots = fmcw::XCD_MAX_SLOTS;
+  {
     CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8));
     CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
     if (!c->x_err.p) {
@@ -757,7 +687,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   int32_t* fix_list = fix_count + 4;
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
   const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
-  if (c->op_gh_scale != p->if_scale || !c->op_gh.p) CHK(build_onepass_gh(c, p->if_scale, s));
+  if (!c->x_tab_ok) CHK(build_xcd_tab(c, s));
   if (pframe >= 0 && d_probe) {                // :410-411 fft_data column: one chirp by a direct DFT
     fmcw::ProbeArgs pa{};
     pa.iq = d_iq; pa.h = h;
@@ -774,8 +704,6 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.rd_scale = h ? 1.0f / ((float)NR * ND) : 1.0f;
     a.F = nf; a.C = C; a.S = S;
     a.calw = c->calw.as<float4>();
-    a.gh = c->op_gh.as<float4>();
-    a.tab = c->op_tab.as<float2>();
     a.tw_nr = c->tw_nr.as<float2>(); a.tw_nd = c->tw_nd.as<float2>(); a.wd = c->wd.as<float>();
     a.rd = d_rd ? static_cast<char*>(d_rd) + (size_t)f0 * NR * ND * (h ? 4 : 8) : nullptr;
     a.profile = d_prof + f0 * NR;
@@ -785,6 +713,8 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
     a.xcube = c->x_cube.as<float2>(); a.xctr = c->x_ctr.as<unsigned>(); a.xerr = c->x_err.as<unsigned>();
     a.slots = slots; a.xtab = c->x_tab.as<float2>(); a.cal_sum = c->cal_sum;
+    a.nteams = c->xcd_teams > 0 ? c->xcd_teams : 0;
+    std::memcpy(a.xcc_team, c->xcc_team, sizeof(a.xcc_team));
     {
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;
@@ -794,24 +724,19 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     if (!xdbg) HIPCHK(hipMalloc(&xdbg, (size_t)1 << 16));
     a.dbg = xdbg;
 #endif
-#ifdef OP_STAMPS
-    static unsigned long long* dbg = nullptr;
-    const size_t nblk = (size_t)((nf + 7) / 8) * 64;
-    if (!dbg) HIPCHK(hipMalloc(&dbg, (size_t)1 << 24));
-    a.dbg = dbg;
-#endif
     {
       StageTimer tm(c, 8, s, 2);
-      if (xcd) {
+      {
         HIPCHK(fmcw::launch_xcd(a, s));
         c->xcd_used = true;
 #ifdef XK_STAMPS
         {   // diagnostic build: per-step phase times of k_rdx (100 MHz realtime clock), averaged over blocks
-          std::vector<unsigned long long> hh(fmcw::XCD_GRID * 8);
+          const int nblk = 32 * a.nteams;
+          std::vector<unsigned long long> hh(nblk * 8);
           HIPCHK(hipStreamSynchronize(s));
           HIPCHK(hipMemcpy(hh.data(), a.dbg, hh.size() * 8, hipMemcpyDeviceToHost));
           double ph[6] = {0, 0, 0, 0, 0, 0}, steps = 0;
-          for (int bb = 0; bb < fmcw::XCD_GRID; ++bb) {
+          for (int bb = 0; bb < nblk; ++bb) {
             for (int q = 0; q < 6; ++q) ph[q] += (double)hh[bb * 8 + q];
             steps += (double)hh[bb * 8 + 6];
           }
@@ -820,56 +745,9 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
                        ph[2] / steps / 100, ph[3] / steps / 100, ph[4] / steps / 100, ph[5] / steps / 100);
         }
 #endif
-      } else {
-        HIPCHK(fmcw::launch_onepass(a, s));
       }
       tm.done();
     }
-#ifdef OP_STAMPS
-    {   // diagnostic build: per-phase durations and concurrency of k_rd1p (100 MHz realtime clock)
-      // stamps: 0 entry, 1 prologue issued, 2 wave 0 range loop done, 3 reductions done,
-      //         4 Doppler stores issued, 5 stores drained
-#ifdef OP_STAMPS2
-      constexpr int NST = 16;
-#else
-      constexpr int NST = 8;
-#endif
-      std::vector<unsigned long long> h(nblk * NST);
-      HIPCHK(hipStreamSynchronize(s));
-      HIPCHK(hipMemcpy(h.data(), dbg, h.size() * 8, hipMemcpyDeviceToHost));
-      unsigned long long lo = ~0ull, hi = 0;
-      double ph[5] = {0, 0, 0, 0, 0};
-      for (size_t i = 0; i < nblk; ++i) {
-        lo = std::min(lo, h[NST * i]); hi = std::max(hi, h[NST * i + 5]);
-        for (int q = 0; q < 5; ++q) ph[q] += (double)(h[NST * i + q + 1] - h[NST * i + q]);
-      }
-      double w4 = 0, w7 = 0;   // range loop end of waves 4 and 7 (stamps 6, 7) after the prologue
-      for (size_t i = 0; i < nblk; ++i) { w4 += (double)(h[NST * i + 6] - h[NST * i + 1]); w7 += (double)(h[NST * i + 7] - h[NST * i + 1]); }
-      std::fprintf(stderr, "stamps-waves: range loop end after prologue (us): wave0 %.2f wave4 %.2f wave7 %.2f\n",
-                   ph[1] / nblk / 100.0, w4 / nblk / 100.0, w7 / nblk / 100.0);
-      const double span = (double)(hi - lo);
-      double life = 0;
-      for (int q = 0; q < 5; ++q) life += ph[q];
-      std::fprintf(stderr, "stamps: blocks %zu span %.1f us | per block us: prologue %.2f range %.2f reduce %.2f "
-                   "doppler %.2f drain %.2f (life %.2f) | avg resident %.1f\n", nblk, span / 100.0,
-                   ph[0] / nblk / 100.0, ph[1] / nblk / 100.0, ph[2] / nblk / 100.0, ph[3] / nblk / 100.0,
-                   ph[4] / nblk / 100.0, life / nblk / 100.0, life / span);
-#ifdef OP_STAMPS2
-      {   // wave 0's timeline from the range loop end: 2 -> B2 8 -> 3 -> 9 -> 10 -> B3 11 -> 12 -> 13 -> B4/B5 14 -> 4 -> 5
-        const int ord[] = {2, 8, 3, 9, 10, 11, 12, 13, 14, 4, 5};
-        const char* nm[] = {"B1+tile1+partials+B2", "reduce", "candidates", "pre0+stage0", "B3", "post0", "pre1",
-                            "B4+stage1+B5", "post1", "drain"};
-        std::string o;
-        for (int q = 0; q < 10; ++q) {
-          double d = 0;
-          for (size_t i = 0; i < nblk; ++i) d += (double)(h[NST * i + ord[q + 1]] - h[NST * i + ord[q]]);
-          o += std::string(nm[q]) + " " + std::to_string(d / nblk / 100.0).substr(0, 5) + " | ";
-        }
-        std::fprintf(stderr, "stamps-doppler (us): %s\n", o.c_str());
-      }
-#endif
-    }
-#endif
     HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
     fmcw::Detect1pArgs k{};
     k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.rd_h = h; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
@@ -917,26 +795,26 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   // the single pass keeps one storage type end to end: c64 in / c64 RD, or
   // fp16 storage (c32h in / c32h RD); the RD dtype is free when RD is not asked for
   const bool onepass_ok = !d_cube && (!d_rd || out_dtype == in_dtype) && fmcw::onepass_supported(S, C, NR, ND);
-  // AUTO = single pass wherever it applies: half the HBM bytes of the streams
-  // schedule (no range cube) and faster on MI355X
-  if (c->pipe_mode == FMCW_PIPE_ONEPASS || c->pipe_mode == FMCW_PIPE_XCD || (c->pipe_mode == FMCW_PIPE_AUTO && onepass_ok)) {
+  // the XCD-team single pass (k_rdx) wherever it applies: half the HBM bytes of the streams
+  // schedule (no range cube) and faster on MI355X; FMCW_PIPE_ONEPASS is
+  // the same schedule (the 8-tile single pass of ABI 2 is retired); AUTO falls back to the
+  // streams schedule where the geometry or the device does not allow it
+  const bool want = c->pipe_mode == FMCW_PIPE_ONEPASS || c->pipe_mode == FMCW_PIPE_XCD;
+  if (want || (c->pipe_mode == FMCW_PIPE_AUTO && onepass_ok)) {
     if (!onepass_ok)
       return fail(FMCW_E_ARG, "single-pass schedule: needs nr 1024, pn == nd == 256, even nts <= nr, "
                               "the RD map in the IQ dtype and no range cube");
-    bool xcd = false;
-    if (c->pipe_mode == FMCW_PIPE_XCD || c->pipe_mode == FMCW_PIPE_AUTO) {
-      if (c->xcd_ok < 0) {
-        int ok = 0;
-        HIPCHK(fmcw::xcd_census(&ok));
-        const char* e = std::getenv("FMCW_NO_XCD");
-        c->xcd_ok = ok && !(e && e[0] == '1');
-      }
-      if (c->pipe_mode == FMCW_PIPE_XCD && !c->xcd_ok)
-        return fail(FMCW_E_ARG, "XCD schedule: needs a 256-CU device that deals a 256-block grid 32 per XCD");
-      xcd = c->xcd_ok == 1;
+    if (c->xcd_teams < 0) {
+      int n = 0;
+      HIPCHK(fmcw::xcd_census(&n, c->xcc_team));
+      const char* e = std::getenv("FMCW_NO_XCD");
+      c->xcd_teams = (e && e[0] == '1') ? 0 : n;
     }
-    return process_onepass(c, p, d_iq, in_dtype == FMCW_C32H ? 1 : 0, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_rd, probe_column,
-                           d_probe, s, xcd);
+    if (c->xcd_teams > 0)
+      return process_onepass(c, p, d_iq, in_dtype == FMCW_C32H ? 1 : 0, F, d_prof, d_count, d_ridx, d_rmag, d_didx,
+                             d_slow, d_rd, probe_column, d_probe, s);
+    if (want)
+      return fail(FMCW_E_ARG, "XCD schedule: needs 32 CUs per XCD and a grid of one workgroup per CU dealt 32 per XCD");
   }
   const int64_t chunk = c->chunk_frames > 0 ? c->chunk_frames : default_chunk(p);
   const int cube_dt = d_cube ? out_dtype : FMCW_C64;

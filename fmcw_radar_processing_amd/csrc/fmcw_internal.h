@@ -62,18 +62,9 @@ struct DetectParams {
   float cube_unscale, rd_unscale;
 };
 
-// Single-pass range+Doppler (kernels_onepass.hip).  Frame f is split into
-// OP_TILES range tiles: tile t owns the bins r == t (mod OP_TILES) for every
-// chirp, held in registers; the range cube never exists in memory.
-constexpr int OP_TILES = 8;
-constexpr int OP_CAND = 2;           // slow-time candidate rows kept per tile
-// Single-pass table (float2), lane-ordered sections:
-constexpr int OP_TAB_LANE = 0;       // [6][64]: DIF twiddles of spans 32..2 (1 on clear lanes of spans 8..2), W128^lane_bin(l)
-constexpr int OP_TAB_TWR = 384;      // [8][32]: W256^(i d2)
-constexpr int OP_TAB_CST = 640;      // [8 t][8 j][2 e][64 l]: w'[n] W1024^(t n), n = 2l + e + 128j
-constexpr int OP_TAB_TWR2 = 640 + 8 * 1024;    // [256 e][32 d2]: W256^(e d2) (rotated chirp order)
-constexpr int OP_TAB_SIZE = OP_TAB_TWR2 + 256 * 32;
-
+// Single-pass range+Doppler (kernels_xcd.hip, k_rdx): the range cube never
+// reaches HBM; k_detect_1p / k_slow_fix / k_probe (kernels_detect.hip) finish
+// the per-frame outputs.
 struct OnePassArgs {
   const void* iq;          // [F][C][S] c64, or c32h when h
   int h;                   // fp16 storage (FMCW_C32H): c32h IQ in, c32h RD out holding D / (NR ND)
@@ -81,21 +72,18 @@ struct OnePassArgs {
   int64_t F;
   int C, S;                // NR = 1024, ND = C (kernel template)
   const float4* calw;      // [S] {cal.re, cal.im, IF_scale*w, w}
-  const float4* gh;        // [8 t][2 s][64 l] {Gh, Hh} of bin t + 8 (lane_bin(l) + 64 s):
-                           // DFT((cal - mean(cal)) w') and DFT(w') (host, float64)
-  const float2* tab;       // OP_TAB_* sections (host, float64, lane order)
   const float2* tw_nr;     // [NR]
   const float2* tw_nd;     // [ND]
   const float* wd;         // [C]
   void* rd;                // [F][NR][ND] c64 (c32h when h), or nullptr (then only the row peaks are kept)
   float* profile;          // [F][NR]
   int2* rowpk;             // [F][NR] {float bits of max_d |D[r,d]|, first argmax d (fftshift-ed, 0-based)}; only when rd is nullptr
-  int32_t* cand_idx;       // [F][OP_TILES][OP_CAND] 0-based bin or -1
-  float* cand_rows;        // [F][OP_TILES][OP_CAND][C] |X[bin, k]|^2
+  int32_t* cand_idx;       // [F][XCD_TILES][XCD_CAND] 0-based bin or -1
+  float* cand_rows;        // [F][XCD_TILES][XCD_CAND][C] |X[bin, k]|^2
   float range_thr, min_d, max_d, dist_per_bin;
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
-  unsigned long long* dbg; // diagnostic builds only (-DOP_STAMPS): [blocks][8] s_memrealtime stamps
+  unsigned long long* dbg; // diagnostic builds only (-DXK_STAMPS): [blocks][8] s_memrealtime stamps
   // XCD-team schedule (k_rdx) only:
   float2* xcube;           // [8 XCDs][slots][XCD_TILES groups][C][32] range-cube hand-off slots
   unsigned* xctr;          // [8 XCDs][2: ready, (unused)][XCD_MAX_SLOTS][32] + [8][32] tickets + the abort word:
@@ -104,6 +92,8 @@ struct OnePassArgs {
                            // got more than 32 blocks (the launch's own abort word lets its grid drain; a later
                            // launch starts with a clear one)
   int slots;               // hand-off slots per XCD (XCD_MAX_SLOTS)
+  int nteams;              // XCDs of the device (teams of 32 CUs): 8 in SPX mode, 1-4 in the partition modes
+  int8_t xcc_team[16];     // HW_REG_XCC_ID -> team index 0..nteams-1, -1 for an XCC not in the device
   const float2* xtab;      // XT_* sections (host, float64, lane order)
   float2 cal_sum;          // sum_{n < S} cal[n]
 };
@@ -114,7 +104,7 @@ struct OnePassArgs {
 constexpr int XCD_TILES = 32;        // range-bin groups per frame (one per team member)
 constexpr int XCD_CAND = 2;          // slow-time candidate rows kept per group
 constexpr int XCD_MAX_SLOTS = 4;
-constexpr int XCD_GRID = 256;        // 8 XCDs x 32 CUs, one persistent workgroup per CU
+constexpr int XCD_GRID = 256;        // at most 8 XCDs x 32 CUs, one persistent workgroup per CU
 constexpr int XCD_TICKETS = 8 * 2 * 32 * XCD_MAX_SLOTS;   // xctr offset of the 8 per-XCD member tickets (128-byte lines)
 constexpr int XCD_ABORT = XCD_TICKETS + 8 * 32;           // xctr offset of the launch's abort word (own line)
 constexpr int XCD_IDLE = XCD_ABORT + 32;                  // xctr offset of [256 CUs][32] words the non-publishing
@@ -140,7 +130,7 @@ struct Detect1pArgs {
   int ND, rd_h;
   const int32_t* cand_idx; // [F][tiles][ncand]
   const float* cand_rows;  // [F][tiles][ncand][C] |X|^2
-  int tiles, ncand;        // OP_TILES (tile = bin mod 8) / OP_CAND, or XCD_TILES (tile = xcd_group) / XCD_CAND
+  int tiles, ncand;        // XCD_TILES (tile = xcd_group) / XCD_CAND
   int nframes, NR, C, M;
   DetectParams det;
   int32_t* count;
@@ -165,10 +155,12 @@ struct SlowFixArgs {
   float* slow_mag;
 };
 
-hipError_t launch_onepass(const OnePassArgs& a, hipStream_t s);
 hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s);
 hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s);
-hipError_t xcd_census(int* ok);      // 1 when the device places block b of a 256-block grid on XCD b mod 8
+// The device's XCD teams: *nteams = its XCDs (0 when the XCD-team schedule cannot run: a CU count
+// that is not 32 per XCD, or a grid of one workgroup per CU not dealt 32 per XCD), xcc_team[16]
+// the team index of each HW_REG_XCC_ID.
+hipError_t xcd_census(int* nteams, int8_t* xcc_team);
 hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s);
 
 struct ProbeArgs {          // fft_data column (:410-411) for the single-pass schedule

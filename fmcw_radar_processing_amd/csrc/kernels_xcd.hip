@@ -69,11 +69,11 @@ using namespace op;
 #else
 #define XK_REF 1
 #endif
-#if defined(XK_RD16)
-#define XK_RD_STORES 8                 // RD stores per lane and row group (16-byte lane-pair stores)
-#else
-#define XK_RD_STORES 16
+#define XK_RD_STORES 16                // RD stores per lane and row group
+#ifndef XK_RD_AUX
+#define XK_RD_AUX 16                   // RD store cache policy: sc1 (A/B: 17 = sc0 sc1, 2 = nt)
 #endif
+constexpr int kRdAux = XK_RD_AUX;
 constexpr int NK = 32;                 // team members (CUs) per XCD
 constexpr int C = 256;                 // chirps = Doppler points
 constexpr int NW = 8;                  // waves per workgroup = chirps per member
@@ -124,6 +124,13 @@ __device__ __forceinline__ void wait_ge(const unsigned* p, unsigned v, unsigned*
   }
 }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
+// c32h bits -> complex fp32.  (Through memcpy: ROCm 7.2 clang folds __builtin_bit_cast(__half2,
+// v.y) of an ext-vector element to the bits of v.x.)
+__device__ __forceinline__ float2 h2f(unsigned b) {
+  __half2 h;
+  __builtin_memcpy(&h, &b, 4);
+  return __half22float2(h);
+}
 
 // s_waitcnt vmcnt(N) for a compile-time N (the k_rdx publish counts; tools/check_vmcnt.py
 // proves them on the built code)
@@ -171,8 +178,9 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   if (tid == 0) {
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    const int xx = (int)(xcc & 7);
-    const int kk = (int)__hip_atomic_fetch_add(a.xctr + XCD_TICKETS + xx * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int xx = a.xcc_team[xcc & 15];   // the census's team index of this XCC
+    int kk = NK;
+    if (xx >= 0) kk = (int)__hip_atomic_fetch_add(a.xctr + XCD_TICKETS + xx * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (kk >= NK) { atomicOr(a.xerr, 2u); atomicOr(a.xctr + XCD_ABORT, 1u); }
     team[0] = xx;
     team[1] = kk;
@@ -180,12 +188,17 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   __syncthreads();
   const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
   if (k >= NK) return;                 // more than 32 blocks on one XCD: its team is short (waits time out)
-  const int nj = a.F > x ? (int)((a.F - x + 7) / 8) : 0;   // frames x + 8 j of this XCD
+  const int T = a.nteams;              // teams (XCDs) of the device: frames x + T j for team x
+  const int nj = a.F > x ? (int)((a.F - x + T - 1) / T) : 0;
   const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
   unsigned* ready = a.xctr + (x * 2 + 0) * 32 * XCD_MAX_SLOTS;
 
   using TP = std::conditional_t<H, h4v, f4v>;
   const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
+  // hand-off slot element: c64, or c32h holding X / Nr (exact power of two) for fp16 storage
+  constexpr int kES = H ? 4 : 8, kGL = H ? 4 : 8;     // bytes per slot element, group loads per thread
+  constexpr int64_t kSlotBytes = (int64_t)NK * C * GP * kES;
+  constexpr float kXS = 1.0f / NR, kXU = (float)NR;
 #ifndef XK_NOREF
   // the reference chirp (chirp 0) of the next frame: one sample pair per thread, loaded one
   // step ahead (before the chirp loads, so the step's vmcnt counts cover it) and put into LDS
@@ -257,7 +270,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const c2 csum_w = refw ? csum : c2{0.f, 0.f};
   const float calk = refw ? 1.f : 0.f;
 #endif
-  auto range = [&](const TP (&xin)[8], c2* __restrict__ slot) __attribute__((always_inline)) {
+  auto range = [&](const TP (&xin)[8], char* __restrict__ slot) __attribute__((always_inline)) {
     c2 v[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -332,44 +345,53 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     const int c = k * NW + w;
     // slot stores are buffer stores (and the only ones in k_rdx): tools/check_vmcnt.py finds them
     // by that to prove, on the built code, that every publish waits for them
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, NK * C * GP * 8, 0x00020000);
-#ifdef XK_SLOT16
-    {   // lane pairs swap one value: the even lane stores positions (p, p + 1) of group e = 0,
-        // the odd lane positions (p - 1, p) of group e = 1, one 16-byte store each
-      const bool odd = lane & 1;
-      const int o4 = (((lane >> 5) * C + c) * GP + (lane & 30) + (odd ? 2 * C * GP : 0)) * 8;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, kSlotBytes, 0x00020000);
+    if constexpr (H) {   // fp16 storage: the slot holds X / Nr as c32h (half the bytes of the hand-off)
+      const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 4;
 #pragma unroll
       for (int s2 = 0; s2 < 8; ++s2) {
-        const c2 snd = odd ? q0[s2] : q1[s2];
-        const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
-        const c2 lo = odd ? rcv : q0[s2], hi = odd ? q1[s2] : rcv;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, f4v{lo.x, lo.y, hi.x, hi.y}), rs,
-                                               o4 + 4 * s2 * C * GP * 8, 0, 0);
+        const __half2 h0 = __floats2half2_rn(q0[s2].x * kXS, q0[s2].y * kXS);
+        const __half2 h1 = __floats2half2_rn(q1[s2].x * kXS, q1[s2].y * kXS);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h0), rs, o + 4 * s2 * C * GP * 4, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h1), rs, o + (4 * s2 + 2) * C * GP * 4, 0, 0);
       }
+      return;
     }
-#else
     const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 8;
 #pragma unroll
     for (int s2 = 0; s2 < 8; ++s2) {
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q0[s2]), rs, o + 4 * s2 * C * GP * 8, 0, 0);
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q1[s2]), rs, o + (4 * s2 + 2) * C * GP * 8, 0, 0);
     }
-#endif
   };
 
   // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259) ----------------
   // buffer_load ... sc1: the CU's L1 is bypassed (no stale lines from the slot's
   // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
-  auto ld_group = [&](const c2* __restrict__ grp, f4v (&t)[8]) __attribute__((always_inline)) {
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<c2*>(grp), (short)0, C * GP * 8, 0x00020000);
+  // (fp16 storage: the group is 32 KiB of c32h, 4 loads per thread, widened and scaled back by Nr
+  // into the same fp32 staging image)
+  auto ld_group = [&](const char* __restrict__ grp, f4v (&t)[8]) __attribute__((always_inline)) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(grp), (short)0, C * GP * kES, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
+    for (int i = 0; i < kGL; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
   };
   auto stage = [&](const f4v (&t)[8]) __attribute__((always_inline)) {
+    if constexpr (H) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e4 = tid + 512 * i;
-      L.u.stg[(e4 >> 4) * 17 + (e4 & 15)] = t[i];
+      for (int i = 0; i < kGL; ++i) {
+        const int e = tid + 512 * i;            // 16-byte piece: chirp e >> 3, positions 4 (e & 7) .. + 3
+        const u4v u = __builtin_bit_cast(u4v, t[i]);
+        const float2 a0 = h2f(u.x), a1 = h2f(u.y), a2 = h2f(u.z), a3 = h2f(u.w);
+        f4v* d = &L.u.stg[(e >> 3) * 17 + (e & 7) * 2];
+        d[0] = f4v{a0.x, a0.y, a1.x, a1.y} * kXU;
+        d[1] = f4v{a2.x, a2.y, a3.x, a3.y} * kXU;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int e4 = tid + 512 * i;
+        L.u.stg[(e4 >> 4) * 17 + (e4 & 15)] = t[i];
+      }
     }
   };
   // D of one frame from its staged group (the caller staged it and synchronised)
@@ -454,37 +476,21 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     stamp(4);
     // :219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)]
     if constexpr (RD) {
-      if constexpr (H) {
-        __half2* __restrict__ out = reinterpret_cast<__half2*>(a.rd) + (f * NR + r) * (int64_t)C + q;
+      // RD rows: buffer stores with the sc1 cache policy (the written lines stream out of the
+      // XCD's L2 instead of evicting the hand-off slots; measured 4.93 -> 4.67 ms per 4096
+      // frames against nontemporal global stores)
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+          static_cast<char*>(a.rd) + f * NR * (int64_t)C * (H ? 4 : 8), (short)0, NR * C * (H ? 4 : 8), 0x00020000);
 #pragma unroll
-        for (int d1s = 0; d1s < 16; ++d1s) {
+      for (int d1s = 0; d1s < 16; ++d1s) {
+        const int off = r * C + q + 16 * d1s;
+        if constexpr (H) {
           const c2 o = xv[(d1s + 8) & 15] * a.rd_scale;
-          out[16 * d1s] = __floats2half2_rn(o.x, o.y);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, __floats2half2_rn(o.x, o.y)), rr, off * 4, 0,
+                                                kRdAux);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, xv[(d1s + 8) & 15]), rr, off * 8, 0, kRdAux);
         }
-      } else {
-#ifdef XK_RD16
-        // lane pairs swap one value per pair of columns: 8 16-byte stores per lane
-        const bool odd = q & 1;
-        f4v* __restrict__ out4 = reinterpret_cast<f4v*>(reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + (q & 14));
-#pragma unroll
-        for (int t = 0; t < 8; ++t) {
-          const c2 ve = xv[(2 * t + 8) & 15], vo = xv[(2 * t + 9) & 15];   // columns 2t, 2t + 1 (fftshift-ed)
-          const c2 snd = odd ? ve : vo;
-          const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
-          const c2 lo = odd ? rcv : ve, hi = odd ? vo : rcv;
-          // even lane: positions (q, q + 1) of column 2t; odd lane: (q - 1, q) of column 2t + 1
-          f4v* dst = out4 + (odd ? 16 * (2 * t + 1) / 2 : 16 * (2 * t) / 2);
-#ifdef XK_RD_WT
-          st_wt(dst, f4v{lo.x, lo.y, hi.x, hi.y});
-#else
-          __builtin_nontemporal_store(f4v{lo.x, lo.y, hi.x, hi.y}, dst);
-#endif
-        }
-#else
-        f2v* __restrict__ out = reinterpret_cast<f2v*>(a.rd) + (f * NR + r) * (int64_t)C + q;
-#pragma unroll
-        for (int d1s = 0; d1s < 16; ++d1s) __builtin_nontemporal_store(xv[(d1s + 8) & 15], out + 16 * d1s);
-#endif
       }
     } else {   // :233 [val, di] = max(abs(.)) of the row: exact max of |D|^2, then its first position
       float m = abs2v(xv[8]);
@@ -500,9 +506,9 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     }
   };
 
-  c2* __restrict__ slots0 = reinterpret_cast<c2*>(a.xcube) + (int64_t)x * NS * (NK * C * GP);
-  auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % NS) * (NK * C * GP); };
-  auto frame = [&](int j) __attribute__((always_inline)) { return x + 8 * (int64_t)j; };
+  char* __restrict__ slots0 = reinterpret_cast<char*>(a.xcube) + (int64_t)x * NS * kSlotBytes;
+  auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % NS) * kSlotBytes; };
+  auto frame = [&](int j) __attribute__((always_inline)) { return x + (int64_t)T * j; };
   // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - NS,
   // and R(j) runs after this member saw ready(j - 2); a member publishes R(j - 2)
   // only after its own reads of frame j - 4 (at most) have returned, so slots >= 4.
@@ -542,7 +548,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       if (lane == 0)
         __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % NS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
                                w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (dj) ld_group(slot(j - 2) + (int64_t)k * C * GP, grp);
+    if (dj) ld_group(slot(j - 2) + (int64_t)k * C * GP * kES, grp);
     stamp(5);
     if (rj) range(xin, slot(j));
     stamp(0);
@@ -588,8 +594,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
 }
 
-// One 256-block grid shaped like k_rdx (512 threads, the same LDS): block b
-// records the XCD it runs on; k_rdx needs 32 blocks on each of the 8 XCDs.
+// A grid of one block per CU shaped like k_rdx (512 threads, the same LDS): block b
+// records the XCD it runs on; k_rdx needs 32 blocks on each of the device's XCDs.
 // (dynamic LDS of sizeof(LdsX): one workgroup per CU, as k_rdx)
 __global__ __launch_bounds__(512, 1) void k_xcd_census(int* out) {
   if (threadIdx.x == 0) {
@@ -628,7 +634,8 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
     if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
   }
   if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
-  const dim3 g(XCD_GRID), bl(64 * xk::NW);
+  if (a.nteams < 1 || a.nteams > 8) return hipErrorInvalidValue;
+  const dim3 g(xk::NK * a.nteams), bl(64 * xk::NW);
   const bool rd = a.rd != nullptr;
   if (a.S == op::NR) {
     if (a.h) {
@@ -651,34 +658,46 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   return hipEventRecord(xcd_chain_ev[dev], s);
 }
 
-hipError_t xcd_census(int* ok) {
-  *ok = 0;
+hipError_t xcd_census(int* nteams, int8_t* xcc_team) {
+  *nteams = 0;
+  for (int i = 0; i < 16; ++i) xcc_team[i] = -1;
   int dev = 0, cus = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e != hipSuccess) return e;
-  if (cus != XCD_GRID) {                    // the team geometry needs 8 XCDs x 32 CUs
-    if (const char* v = std::getenv("FMCW_XCD_DEBUG"); v && v[0] == '1') std::fprintf(stderr, "xcd_census: %d CUs\n", cus);
+  const bool dbg = [] { const char* v = std::getenv("FMCW_XCD_DEBUG"); return v && v[0] == '1'; }();
+  // 32 CUs per XCD: 256 in SPX mode, 128 / 64 / 32 per device in the DPX / QPX / CPX partition modes
+  if (cus < xk::NK || cus > XCD_GRID || cus % xk::NK) {
+    if (dbg) std::fprintf(stderr, "xcd_census: %d CUs\n", cus);
     return hipSuccess;
   }
   int* d = nullptr;
   if ((e = hipMalloc(&d, XCD_GRID * sizeof(int))) != hipSuccess) return e;
   int h[XCD_GRID];
-  hipLaunchKernelGGL(k_xcd_census, dim3(XCD_GRID), dim3(512), sizeof(xk::LdsX), 0, d);
+  hipLaunchKernelGGL(k_xcd_census, dim3(cus), dim3(512), sizeof(xk::LdsX), 0, d);
   e = hipGetLastError();
-  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(int) * cus, hipMemcpyDeviceToHost);
   (void)hipFree(d);
   if (e != hipSuccess) return e;
-  int n[8] = {}, good = 1;
-  for (int b = 0; b < XCD_GRID; ++b) {
-    if (h[b] < 0 || h[b] > 7) good = 0;
+  int n[16] = {};
+  bool good = true;
+  for (int b = 0; b < cus; ++b) {
+    if (h[b] < 0 || h[b] > 15) good = false;
     else ++n[h[b]];
   }
-  for (int i = 0; i < 8; ++i) good &= n[i] == XCD_GRID / 8;
-  *ok = good;
-  if (const char* v = std::getenv("FMCW_XCD_DEBUG"); v && v[0] == '1') {
-    std::fprintf(stderr, "xcd_census: cus %d ok %d, XCC of blocks 0..15:", cus, good);
-    for (int b = 0; b < 16; ++b) std::fprintf(stderr, " %d", h[b]);
+  int t = 0;
+  for (int i = 0; i < 16 && good; ++i) {
+    if (n[i] == 0) continue;
+    if (n[i] != xk::NK) good = false;     // every XCD of the device must hold exactly one team
+    else xcc_team[i] = (int8_t)t++;
+  }
+  good = good && t * xk::NK == cus;
+  if (good) *nteams = t;
+  else
+    for (int i = 0; i < 16; ++i) xcc_team[i] = -1;
+  if (dbg) {
+    std::fprintf(stderr, "xcd_census: cus %d teams %d, XCC of blocks 0..15:", cus, *nteams);
+    for (int b = 0; b < 16 && b < cus; ++b) std::fprintf(stderr, " %d", h[b]);
     std::fprintf(stderr, "\n");
   }
   return hipSuccess;

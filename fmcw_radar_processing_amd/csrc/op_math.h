@@ -1,7 +1,7 @@
-// op_math.h -- register-level building blocks shared by the single-pass kernels
-// (kernels_onepass.hip: k_rd1p, 8 range tiles per frame; kernels_xcd.hip: k_rdx,
-// the chirp-split XCD-team schedule): packed complex MACs with op_sel modifiers,
-// DPP / permlane lane exchanges, wave reductions and the packed small DFTs.
+// op_math.h -- register-level building blocks of the single-pass schedule
+// (kernels_xcd.hip: k_rdx, the chirp-split XCD-team schedule; kernels_detect.hip):
+// packed complex multiplies with op_sel modifiers, DPP / permlane lane exchanges,
+// wave reductions and the packed small DFTs.
 #pragma once
 #include "frame_ops.h"
 
@@ -21,45 +21,18 @@ __device__ __forceinline__ float2 ld_iq(const void* p, int64_t i, int h) {
 
 // a * b in two packed ops: a.re * (b.re, b.im) + a.im * (-b.im, b.re)
 __device__ __forceinline__ c2 cmv(c2 a, c2 b) { return __builtin_elementwise_fma(a.yy, c2{-b.y, b.x}, a.xx * b); }
-// acc + a * b given bs = (-b.im, b.re)
-__device__ __forceinline__ c2 cmacv(c2 acc, c2 a, c2 b, c2 bs) {
-  return __builtin_elementwise_fma(a.yy, bs, __builtin_elementwise_fma(a.xx, b, acc));
-}
-// acc + a * b and a * b against a per-lane VGPR constant b: the rotation of b
-// is done by operand modifiers (op_sel picks b.im for the low half, neg_lo
-// negates it), so no rotated copy of b is kept.  Results must not feed a
-// DPP / permlane op directly (the hazard recognizer does not see inline asm).
-__device__ __forceinline__ c2 cmac_a(c2 acc, c2 a, c2 b) {
-  c2 t, r;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1]" : "=v"(t) : "v"(a), "v"(b), "v"(acc));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
-  return r;
-}
+// a * b against a per-lane VGPR constant b: the rotation of b is done by operand
+// modifiers (op_sel picks b.im for the low half, neg_lo negates it), so no rotated
+// copy of b is kept.  Results must not feed a DPP / permlane op directly (the
+// hazard recognizer does not see inline asm).
 __device__ __forceinline__ c2 cmul_a(c2 a, c2 b) {
   c2 t, r;
   asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(t));
   return r;
 }
-// 16-byte / 8-byte write-through store (global_store ... sc0 sc1): the line leaves the XCD's L2
-#ifdef OP_RD_PLAIN
-__device__ __forceinline__ void st_wt(f4v* p, f4v v) { *p = v; }
-__device__ __forceinline__ void st_wt(h4v* p, h4v v) { *p = v; }
-#else
-// The s_nop covers the store-data hazard the compiler cannot see through inline asm: a
-// VALU write to the data VGPRs of a > 8-byte VMEM store right after it needs wait states
-// (without it the next lane-pair exchange overwrote the data before the store read it).
-__device__ __forceinline__ void st_wt(f4v* p, f4v v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_wt(h4v* p, h4v v) {
-  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
-}
-#endif
 __device__ __forceinline__ c2 tov(float2 v) { return c2{v.x, v.y}; }
-__device__ __forceinline__ float2 tof(c2 v) { return make_float2(v.x, v.y); }
 __device__ __forceinline__ float abs2v(c2 v) { return fmaf(v.x, v.x, v.y * v.y); }
-__device__ __forceinline__ c2 mnegi(c2 a) { return c2{a.y, -a.x}; }   // a * (-i)
 // a + (-i) b = (a.re + b.im, a.im - b.re) and a + i b = (a.re - b.im, a.im + b.re) as ONE
 // v_pk_add_f32 (op_sel swaps b's halves, neg_* flips one of them): the compiler would
 // build the rotated b with moves and sign flips first.  Not fed to DPP/permlane (the
@@ -84,13 +57,6 @@ template <int CTRL> __device__ __forceinline__ int dppi(int v) {
   return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
 }
 
-// Value of lane ^ H, H < 16, by DPP (FFT data: not uniform inside groups).
-template <int H> __device__ __forceinline__ float xpart(float v) {
-  if constexpr (H == 1) return dppf<0xB1>(v);            // quad_perm [1,0,3,2]
-  if constexpr (H == 2) return dppf<0x4E>(v);            // quad_perm [2,3,0,1]
-  if constexpr (H == 8) return dppf<0x128>(v);           // row_ror:8 == xor 8 inside a row
-  return dppf<0x1B>(dppf<0x141>(v));                     // row_half_mirror (7-i), then quad_perm [3,2,1,0]: i ^ 4
-}
 // (value of the bit-H-clear lane, value of the bit-H-set lane) of this lane's pair, H = 16, 32
 template <int H> __device__ __forceinline__ void xhalves(float v, float& lo, float& hi) {
   if constexpr (H == 32) {   // lanes 32-63 of the first operand swap with lanes 0-31 of the second
@@ -140,61 +106,6 @@ __device__ __forceinline__ void wave_argmax_dpp(float& v, int& i) {
   const int m = wave_red_i<true>(key);
   i = wave_red_i<false>(key == m ? i : INT_MAX);
   v = m < 0 ? -1.f : __int_as_float(m);
-}
-
-// One radix-2 DIF stage of span H across lanes: bit-H-clear lane -> a + b,
-// bit-H-set lane -> (a - b) * tw.  sg = -1 on set lanes, +1 on clear lanes.
-template <int H>
-__device__ __forceinline__ c2 dif_stage(c2 x, c2 tw, float sg) {
-  c2 u;
-  if constexpr (H >= 16) {
-    float lr, hr, li, hi;
-    xhalves<H>(x.x, lr, hr);
-    xhalves<H>(x.y, li, hi);
-    u = __builtin_elementwise_fma(c2{sg, sg}, c2{hr, hi}, c2{lr, li});
-  } else {
-    const c2 o = c2{xpart<H>(x.x), xpart<H>(x.y)};               // the partner's value
-    u = __builtin_elementwise_fma(c2{sg, sg}, x, o);              // clear: o + x, set: o - x
-  }
-  return H == 1 ? u : cmv(u, tw);
-}
-
-// Wave-uniform table read through the constant address space: an s_load into
-// SGPRs instead of a vector load into VGPRs (the index must be wave-uniform).
-__device__ __forceinline__ float sload(const float* p, int i) {
-  return ((const __attribute__((address_space(4))) float*)p)[i];
-}
-__device__ __forceinline__ float2 sload(const float2* p, int i) {
-  const f2v v = ((const __attribute__((address_space(4))) f2v*)p)[i];
-  return make_float2(v.x, v.y);
-}
-
-// Sub-bin m (r = t + 8 m) of lane l's slot-0 value after the range FFT below:
-// 4 bitrev4(l mod 16) + l / 16 (the two pair stages leave the four 16-point
-// sub-FFTs of each half-sequence in the four 16-lane rows).
-__device__ __forceinline__ int lane_bin(int l) { return (int)(__brev((unsigned)(l & 15)) >> 26) + (l >> 4); }
-
-// Pair butterfly of span H (32 or 16) on two registers: one half swap per
-// component gives every lane both operands of one butterfly (no copies), and it
-// keeps both outputs: R0 <- lo + hi, R1 <- (lo - hi) * tw.  Lane l < H-block
-// handles R0's pair, the other block R1's pair (see lane_bin).
-template <int H> __device__ __forceinline__ void pair_bfly(c2& R0, c2& R1, c2 tw) {
-  const auto rx = H == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.x), __float_as_uint(R1.x), false, false)
-                          : __builtin_amdgcn_permlane16_swap(__float_as_uint(R0.x), __float_as_uint(R1.x), false, false);
-  const auto ry = H == 32 ? __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.y), __float_as_uint(R1.y), false, false)
-                          : __builtin_amdgcn_permlane16_swap(__float_as_uint(R0.y), __float_as_uint(R1.y), false, false);
-  const c2 lo = c2{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
-  const c2 hi = c2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
-  R0 = lo + hi;
-  R1 = cmv(lo - hi, tw);
-}
-// The final half swap without arithmetic: lane l then holds (E[m], O[m]) of
-// one sub-bin m = lane_bin(l).
-__device__ __forceinline__ void pair_swap32(c2& R0, c2& R1) {
-  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.x), __float_as_uint(R1.x), false, false);
-  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(R0.y), __float_as_uint(R1.y), false, false);
-  R0 = c2{__uint_as_float(rx[0]), __uint_as_float(ry[0])};
-  R1 = c2{__uint_as_float(rx[1]), __uint_as_float(ry[1])};
 }
 
 // Wave-wide complex sum, every lane gets it.  The 16-lane swap of re against im
@@ -272,36 +183,5 @@ __device__ __forceinline__ void dft16p(c2* v) {
     v[STRIDE * k1] = a0; v[STRIDE * (k1 + 4)] = a1; v[STRIDE * (k1 + 8)] = a2; v[STRIDE * (k1 + 12)] = a3;
   }
 }
-// 32 points, in place: radix-2 DIT over the even / odd dft16p (stride 2).
-__device__ __forceinline__ void dft32p(c2 (&v)[32]) {
-  constexpr float kc[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
-                            0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
-                            0.19509032201612826785f, 0.0f, -0.19509032201612826785f, -0.38268343236508977173f,
-                            -0.55557023301960222474f, -0.70710678118654752440f, -0.83146961230254523708f,
-                            -0.92387953251128675613f, -0.98078528040323044913f};
-  constexpr float ks[16] = {0.0f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
-                            0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
-                            0.98078528040323044913f, 1.0f, 0.98078528040323044913f, 0.92387953251128675613f,
-                            0.83146961230254523708f, 0.70710678118654752440f, 0.55557023301960222474f,
-                            0.38268343236508977173f, 0.19509032201612826785f};
-  dft16p<2>(v);                                  // evens: v[2k] = E[k]
-  dft16p<2>(v + 1);                              // odds:  v[2k+1] = O[k]
-  c2 r[32];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const c2 e = v[2 * k];
-    if (k == 8) {                                // W32^8 O[8] = -i O[8]
-      r[k] = add_mi(e, v[17]);
-      r[k + 16] = add_pi(e, v[17]);
-      continue;
-    }
-    const c2 ot = k == 0 ? v[1] : cmv(v[2 * k + 1], c2{kc[k], -ks[k]});   // W32^k O[k]
-    r[k] = e + ot;
-    r[k + 16] = e - ot;
-  }
-#pragma unroll
-  for (int k = 0; k < 32; ++k) v[k] = r[k];
-}
-
 }  // namespace op
 }  // namespace fmcw

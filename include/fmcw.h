@@ -238,7 +238,7 @@ int fmcw_synth_device(fmcw_ctx* ctx, const fmcw_params* p, int64_t frame0, int64
  * Doppler launch; the chunks run as a 3-stream software pipeline) and one pair
  * per STFT-side launch (stages 3-6); 2 = additionally one pair per K1/K2/K3.
  * stage: 0 range, 1 doppler, 2 detect, 3 compact, 4 stft_power, 5 stft_db,
- *        6 range_only, 7 range+Doppler span, 8 k_rd1p (single-pass schedule,
+ *        6 range_only, 7 range+Doppler span, 8 k_rdx (single-pass schedule,
  *        level 2), 9 render (spectrogram.png).  fmcw_timing_read synchronises. */
 int fmcw_timing_enable(fmcw_ctx* ctx, int32_t enable);
 int fmcw_timing_read(fmcw_ctx* ctx, int32_t stage, double* total_ms, int64_t* launches);
@@ -250,27 +250,26 @@ int fmcw_timing_reset(fmcw_ctx* ctx);
 int fmcw_set_chunk_frames(fmcw_ctx* ctx, int64_t frames);
 
 /* Schedule of fmcw_process_device / fmcw_process (the two agree to fp32 rounding):
- *  FMCW_PIPE_AUTO    a single-pass schedule where it applies (geometry below, no
- *                    range cube requested), else the streams schedule;
+ *  FMCW_PIPE_AUTO    the single-pass XCD-team schedule where it applies (geometry
+ *                    and device below, no range cube requested), else the streams
+ *                    schedule;
  *  FMCW_PIPE_STREAMS K1 | K2 | K3 kernels as a 3-stream chunk pipeline, the
  *                    range cube of each chunk round-trips through HBM;
- *  FMCW_PIPE_ONEPASS single pass per frame (kernels_onepass.hip): 8 range tiles
- *                    per frame, each keeping its bins (r == t mod 8) of every
- *                    chirp in registers/LDS through the Doppler FFT, so the
- *                    range cube never reaches memory.  Needs nr 1024,
- *                    pn == nd == 256, even nts <= nr, the RD map (if any) in the
- *                    IQ dtype (complex64 or fp16 storage), no range cube (else E_ARG).
- *  FMCW_PIPE_XCD     the XCD-team schedule (kernels_xcd.hip): the same geometry
- *                    and outputs as FMCW_PIPE_ONEPASS, but the 32 CUs of each XCD
- *                    share a frame (range FFT split by chirps, Doppler FFT by
+ *  FMCW_PIPE_XCD     the XCD-team single pass (kernels_xcd.hip): the 32 CUs of each
+ *                    XCD share a frame (range FFT split by chirps, Doppler FFT by
  *                    range-bin groups, the cube handed over in the XCD's L2), so
- *                    every input byte is read once.  One persistent workgroup per
- *                    CU: needs a 256-CU device that deals a 256-block grid 32
- *                    per XCD (checked once per context, else E_ARG); a hand-off that does
- *                    not complete within ~1 s is reported by fmcw_synchronize
- *                    (and the host-pointer calls) as FMCW_E_HIP.
- * AUTO picks FMCW_PIPE_XCD where it applies and the device passes the check,
- * else FMCW_PIPE_ONEPASS where that applies.
+ *                    every input byte is read once and the range cube never goes
+ *                    to HBM.  Needs nr 1024, pn == nd == 256, even nts <= nr, the RD
+ *                    map (if any) in the IQ dtype (complex64 or fp16 storage), no
+ *                    range cube (else E_ARG).  One persistent workgroup per CU: needs
+ *                    32 CUs per XCD and a grid of one workgroup per CU dealt 32 per
+ *                    XCD -- any XCD count, so the SPX mode (8 XCDs) and the DPX /
+ *                    QPX / CPX partition modes (4 / 2 / 1 XCDs per device) alike;
+ *                    checked once per context by a census, else E_ARG.  A hand-off
+ *                    that does not complete within ~1 s is reported by
+ *                    fmcw_synchronize (and the host-pointer calls) as FMCW_E_HIP.
+ *  FMCW_PIPE_ONEPASS the same as FMCW_PIPE_XCD (ABI 2's 8-tile single pass, which
+ *                    re-read every frame from L2 8 times, is retired).
  * (Value 2 is retired: the persistent "fused" schedule of ABI 1, slower than both.) */
 enum { FMCW_PIPE_AUTO = 0, FMCW_PIPE_STREAMS = 1, FMCW_PIPE_ONEPASS = 3, FMCW_PIPE_XCD = 4 };
 int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode);

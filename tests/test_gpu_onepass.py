@@ -1,10 +1,11 @@
-"""GPU: the single-pass schedule (FMCW_PIPE_ONEPASS, kernels_onepass.hip)
-against the float64 oracle and against the streams schedule.
+"""GPU: the single-pass XCD-team schedule (FMCW_PIPE_XCD, kernels_xcd.hip k_rdx +
+kernels_detect.hip) against the float64 oracle and against the streams schedule.
 
-The single-pass kernel computes each range bin by decimation in frequency
-(8 tiles per frame) instead of the Stockham FFT of k_range, so it agrees with
-the streams schedule to fp32 rounding, not bit for bit; both are held to the
-SURVEY.md 8d tolerances against the oracle.
+k_rdx computes the range FFT as DFT8 x DFT16 x DFT8 with the frame's reference chirp
+subtracted (static-target cancellation) instead of the Stockham FFT of k_range, so it
+agrees with the streams schedule to fp32 rounding, not bit for bit; both are held to
+the SURVEY.md 8d tolerances against the oracle.  FMCW_PIPE_ONEPASS names the same
+schedule (ABI 2's 8-tile single pass is retired).
 """
 import numpy as np
 import pytest
@@ -23,8 +24,8 @@ def _frames(F, nts=1024, frame0=0):
     return cfg, p, wr, wd, cal, iq
 
 
-# both single-pass schedules: 8 range tiles per frame (k_rd1p) and the XCD team (k_rdx)
-@pytest.fixture(params=[FMCW_PIPE_ONEPASS, FMCW_PIPE_XCD], ids=["tiles8", "xcd"])
+# the single-pass schedule, by both of its names (FMCW_PIPE_ONEPASS is FMCW_PIPE_XCD since ABI 3)
+@pytest.fixture(params=[FMCW_PIPE_XCD], ids=["xcd"])
 def onepass(engine, request):
     engine.set_pipeline(request.param)
     yield engine
@@ -190,14 +191,16 @@ def test_onepass_fp16_storage(onepass, monkeypatch, F, nts, fix):
     x = iq16.astype(np.float32).view(np.complex64)[..., 0]
     ref = O.process_frames(x, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
     assert rd_rel_err(got["rd"], ref["rd"], ref["cube"], wd, 256).max() <= TOL_FP16_REL_L2
-    # profile, slow row and detections come from fp32 values: the fp32 bars
-    assert rel_l2(got["profile"], ref["profile"], axis=1).max() <= TOL_FP32_REL_L2
-    ok = ~near_tie_frames(ref["profile"])
+    # profile and slow rows: the fp16-storage bar (the XCD schedule hands the range cube over
+    # as c32h; the 8-tile single pass keeps it in fp32 registers); detections exact except
+    # frames whose two strongest bins are within fp16 rounding of each other
+    assert rel_l2(got["profile"], ref["profile"], axis=1).max() <= TOL_FP16_REL_L2
+    ok = ~near_tie_frames(ref["profile"], rtol=1e-3)
     for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
         np.testing.assert_array_equal(got[k][ok], ref[k][ok], err_msg=k)
     has = ref["tgt_count"] > 0
     assert has.sum() >= 1
-    assert rel_l2(got["slow_mag"][has], ref["slow_mag"][has], axis=1).max() <= TOL_FP32_REL_L2
+    assert rel_l2(got["slow_mag"][has], ref["slow_mag"][has], axis=1).max() <= TOL_FP16_REL_L2
     assert np.all(got["slow_mag"][~has] == 0)
 
 
@@ -222,12 +225,10 @@ def test_onepass_fp16_matches_streams_fp16(engine):
 
 
 # ---- the XCD-team schedule (kernels_xcd.hip) on its own ----------------------
-@pytest.mark.parametrize("slots", ["4"])
-def test_xcd_slot_ring(engine, monkeypatch, slots):
-    """Frames 8 per XCD step: 75 frames = 9-10 steps per team, so every slot of
-    the hand-off ring is reused several times; outputs equal the 8-tile single
-    pass to fp32 rounding and the oracle within the fp32 bars, for any ring depth."""
-    monkeypatch.setenv("FMCW_XCD_SLOTS", slots)
+def test_xcd_slot_ring(engine):
+    """One frame per XCD and step: 75 frames = 9-10 steps per team, so every slot of
+    the hand-off ring is reused several times; the oracle's fp32 bars hold, and
+    FMCW_PIPE_ONEPASS (the same schedule) gives bit-identical outputs."""
     F = 75
     cfg, p, wr, wd, cal, iq = _frames(F, frame0=5000)
     engine.set_taps(cfg, cal, wr, wd)
@@ -241,9 +242,8 @@ def test_xcd_slot_ring(engine, monkeypatch, slots):
         engine.set_pipeline(FMCW_PIPE_AUTO)
     ref = O.process_frames(iq, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
     _check_vs_oracle(cfg, a, ref, wd, F * 256)
-    for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):
+    for k in a:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-    assert rel_l2(a["rd"], b["rd"], axis=(1, 2)).max() <= 2 * TOL_FP32_REL_L2
 
 
 def test_xcd_deterministic_and_chunked(engine):

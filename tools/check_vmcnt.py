@@ -11,8 +11,8 @@ at least N vector-memory operations were issued after it and before the wait.
 
 This script reads the gfx950 assembly of every k_rdx instantiation and checks,
 on every control-flow path into every no-return ``global_atomic_add`` (the
-publishes), that each slot store -- a ``buffer_store_*``; k_rdx issues no other
-buffer stores -- is covered by some wait on the way: between the store and
+publishes), that each slot store -- a ``buffer_store_*`` without a cache-policy
+flag; k_rdx issues no other such stores -- is covered by some wait on the way: between the store and
 that wait at least N vector-memory operations were issued.  A path with no
 slot store (the first steps) is fine.  Calls are treated as issuing nothing
 and waiting for nothing (conservative).  Exit status 1 on any uncovered path:
@@ -64,6 +64,13 @@ def blocks(lines):
     return bl
 
 
+def is_slot_store(ins: str) -> bool:
+    if not ins.startswith("buffer_store"):
+        return False
+    flags = ins.split()[1:]
+    return not any(f in ("sc0", "sc1", "nt", "glc", "slc") for f in flags)
+
+
 def is_vmem(ins: str) -> bool:
     op = ins.split()[0]
     return op.startswith(("global_", "buffer_", "scratch_", "flat_")) and op not in ("buffer_inv",)
@@ -96,7 +103,7 @@ def check_function(name, lines, quiet=False):
     pred = cfg(bl)
     pubs = [(b, k) for b, (_, ins) in enumerate(bl) for k, s in enumerate(ins)
             if s.startswith("global_atomic_add") and " sc0" not in s and " glc" not in s]
-    stores = sum(1 for _, ins in bl for s in ins if s.startswith("buffer_store"))
+    stores = sum(1 for _, ins in bl for s in ins if is_slot_store(s))
     bad = []
     worst = {}
     for b0, k0 in pubs:
@@ -113,7 +120,7 @@ def check_function(name, lines, quiet=False):
                 m = RE_VMCNT.search(s) if s.startswith("s_waitcnt") else None
                 if m:
                     rem = min(rem, int(m.group(1)))
-                if s.startswith("buffer_store"):
+                if is_slot_store(s):
                     if rem > 0:
                         bad.append((bl[b0][0], bl[b][0], rem, path + (bl[b][0],)))
                     worst[(b0, k0)] = max(worst.get((b0, k0), -INF), rem)

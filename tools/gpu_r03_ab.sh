@@ -34,3 +34,10 @@ for i in $(seq $N); do
     grep "^k1" gpurun_out/k1_$n.log
   done
 done
+for i in $(seq $N); do
+  for n in ${FP16NAMES:-}; do
+    echo -n "$n fp16: "
+    FP16=1 FMCW_LIB=ab/$n.so timeout -k 10 120 python -u tools/onepass_perf.py 4096 20 xcd > gpurun_out/ab16_$n.log 2>&1 || { tail -5 gpurun_out/ab16_$n.log; exit 1; }
+    grep -E "^xcd| onepass " gpurun_out/ab16_$n.log | tr -s ' ' | tr '\n' ' '; echo
+  done
+done

@@ -20,7 +20,7 @@ def load(prefix):
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in rows:
             k = r["Kernel_Name"]
-            if "k_rdx" in k or "k_rd1p" in k:
+            if "k_rdx" in k:
                 per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
                 name = k
         big = max(per.values(), key=lambda v: sum(v.values()))

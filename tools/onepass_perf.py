@@ -10,7 +10,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from fmcw_radar_processing_amd import FMCW_C64, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS, FMCW_PIPE_XCD  # noqa: E402
+from fmcw_radar_processing_amd import FMCW_C32H, FMCW_C64, FMCW_PIPE_ONEPASS, FMCW_PIPE_STREAMS, FMCW_PIPE_XCD  # noqa: E402
 from fmcw_radar_processing_amd import params as P  # noqa: E402
 from fmcw_radar_processing_amd.engine import Engine  # noqa: E402
 
@@ -21,33 +21,37 @@ def main(F=4096, reps=10, which="streams,onepass"):
     e.set_taps(cfg, P.synth_calibration(cfg.nts))
     dev = "cuda"
     s = torch.cuda.current_stream()
-    d_iq = torch.empty((F, cfg.pn, cfg.nts, 2), dtype=torch.float32, device=dev)
-    e.synth_device(d_iq, 0, F, FMCW_C64, stream=s)
+    fp16 = os.environ.get("FP16", "0") == "1"          # config-4 fp16 storage: c32h in, c32h RD out
+    dt = FMCW_C32H if fp16 else FMCW_C64
+    tdt = torch.float16 if fp16 else torch.float32
+    d_iq = torch.empty((F, cfg.pn, cfg.nts, 2), dtype=tdt, device=dev)
+    e.synth_device(d_iq, 0, F, dt, stream=s)
     M = cfg.max_targets
     outs = dict(profile=torch.empty((F, cfg.nr), device=dev), tgt_count=torch.empty(F, dtype=torch.int32, device=dev),
                 tgt_range_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
                 tgt_range_mag=torch.empty((F, M), device=dev),
                 tgt_doppler_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
                 slow_mag=torch.empty((F, cfg.pn), device=dev))
-    d_rd = torch.empty((F, cfg.nr, cfg.nd, 2), dtype=torch.float32, device=dev)
-    byt = F * (cfg.pn * cfg.nts * 8 + cfg.nr * cfg.nd * 8 + cfg.nr * 4 + cfg.pn * 4)
+    d_rd = torch.empty((F, cfg.nr, cfg.nd, 2), dtype=tdt, device=dev)
+    es = 4 if fp16 else 8
+    byt = F * (cfg.pn * cfg.nts * es + cfg.nr * cfg.nd * es + cfg.nr * 4 + cfg.pn * 4)
     modes = {"streams": FMCW_PIPE_STREAMS, "onepass": FMCW_PIPE_ONEPASS, "xcd": FMCW_PIPE_XCD}
     for name in which.split(","):
         mode = modes[name]
         e.set_pipeline(mode)
-        e.process_device(d_iq, F, FMCW_C64, outs, d_rd=d_rd, stream=s)
+        e.process_device(d_iq, F, dt, outs, d_rd=d_rd, out_dtype=dt, stream=s)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            e.process_device(d_iq, F, FMCW_C64, outs, d_rd=d_rd, stream=s)
+            e.process_device(d_iq, F, dt, outs, d_rd=d_rd, out_dtype=dt, stream=s)
         torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / reps
-        print(f"{name:8s} F={F}: {dt * 1e3:.3f} ms  {F / dt / 1e6:.3f} Mframes/s  alg {byt / dt / 1e12:.2f} TB/s "
-              f"(frac {byt / dt / 8e12:.3f})", flush=True)
+        el = (time.perf_counter() - t0) / reps
+        print(f"{name + ('16' if fp16 else ''):8s} F={F}: {el * 1e3:.3f} ms  {F / el / 1e6:.3f} Mframes/s  alg {byt / el / 1e12:.2f} TB/s "
+              f"(frac {byt / el / 8e12:.3f})", flush=True)
         e.timing(2)
         e.timing_reset()
         for _ in range(reps):
-            e.process_device(d_iq, F, FMCW_C64, outs, d_rd=d_rd, stream=s)
+            e.process_device(d_iq, F, dt, outs, d_rd=d_rd, out_dtype=dt, stream=s)
         tm = e.timing_read()
         e.timing(0)
         for k, (ms, n) in tm.items():

@@ -20,7 +20,7 @@ def short(name):
 
 def load_counters(path):
     """Per kernel name, the dispatches of its LARGEST grid only (a kernel launched at
-    several sizes, e.g. k_rd1p for the 4096-frame step and for a small host-path
+    several sizes, e.g. k_rdx for the 4096-frame step and for a small host-path
     chunk, would otherwise average unlike launches)."""
     rows = list(csv.DictReader(open(path)))
     big = collections.defaultdict(int)
@@ -53,7 +53,7 @@ def trace_avg_us(path):
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
 
-LABELS = ("k_range", "k_doppler", "k_detect_1p", "k_detect", "k_rd1p", "k_slow_fix", "k_rd_fused", "k_compact", "k_stft_power", "k_stft_db")
+LABELS = ("k_range", "k_doppler", "k_detect_1p", "k_detect", "k_rdx", "k_slow_fix", "k_rd_fused", "k_compact", "k_stft_power", "k_stft_db")
 
 
 def label(k):
