@@ -721,7 +721,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     }
 #ifdef XK_STAMPS
     static unsigned long long* xdbg = nullptr;
-    if (!xdbg) HIPCHK(hipMalloc(&xdbg, (size_t)1 << 16));
+    if (!xdbg) HIPCHK(hipMalloc(&xdbg, (size_t)1 << 17));
     a.dbg = xdbg;
 #endif
     {
@@ -732,17 +732,24 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
 #ifdef XK_STAMPS
         {   // diagnostic build: per-step phase times of k_rdx (100 MHz realtime clock), averaged over blocks
           const int nblk = 32 * a.nteams;
-          std::vector<unsigned long long> hh(nblk * 8);
+          std::vector<unsigned long long> hh(nblk * 32);
           HIPCHK(hipStreamSynchronize(s));
           HIPCHK(hipMemcpy(hh.data(), a.dbg, hh.size() * 8, hipMemcpyDeviceToHost));
-          double ph[6] = {0, 0, 0, 0, 0, 0}, steps = 0;
-          for (int bb = 0; bb < nblk; ++bb) {
-            for (int q = 0; q < 6; ++q) ph[q] += (double)hh[bb * 8 + q];
-            steps += (double)hh[bb * 8 + 6];
+          static const char* nm[10] = {"B1", "poll+stage", "B2", "rows", "pubwait+B3", "grp+cand", "R1+ld+D3",
+                                       "TD+T1+DFT16", "R2+T2+R3", "RD"};
+          for (int wv = 0; wv < 2; ++wv) {
+            double ph[10] = {}, steps = 0;
+            for (int bb = 0; bb < nblk; ++bb) {
+              for (int q = 0; q < 10; ++q) ph[q] += (double)hh[(bb * 2 + wv) * 16 + q];
+              steps += (double)hh[(bb * 2 + wv) * 16 + 15];
+            }
+            double tot = 0;
+            std::fprintf(stderr, "xk-stamps wave %d (us/step):", wv * 4);
+            for (int q = 0; q < 10; ++q) { std::fprintf(stderr, " %s %.2f |", nm[q], ph[q] / steps / 100); tot += ph[q]; }
+            double cyc = 0, rt = 0;
+            for (int bb = 0; bb < nblk; ++bb) { cyc += (double)hh[(bb * 2 + wv) * 16 + 13]; rt += (double)hh[(bb * 2 + wv) * 16 + 14]; }
+            std::fprintf(stderr, " sum %.2f | clock %.3f GHz\n", tot / steps / 100, rt > 0 ? cyc / rt * 0.1 : 0.0);
           }
-          std::fprintf(stderr, "xk-stamps (us per step): range %.2f | drain+publish+prefetch %.2f | ready-wait %.2f | "
-                       "group load+stage %.2f | doppler %.2f | RD stores %.2f\n", ph[0] / steps / 100, ph[1] / steps / 100,
-                       ph[2] / steps / 100, ph[3] / steps / 100, ph[4] / steps / 100, ph[5] / steps / 100);
         }
 #endif
       }

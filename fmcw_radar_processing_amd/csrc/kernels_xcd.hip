@@ -70,6 +70,11 @@ using namespace op;
 #define XK_REF 1
 #endif
 #define XK_RD_STORES 16                // RD stores per lane and row group
+#ifdef XK_SLOT16
+constexpr bool kSlot16 = true;         // A/B only: fp16 hand-off slots under fp16 storage (fails the STFT bar, below)
+#else
+constexpr bool kSlot16 = false;
+#endif
 #ifndef XK_RD_AUX
 #define XK_RD_AUX 16                   // RD store cache policy: sc1 (A/B: 17 = sc0 sc1, 2 = nt)
 #endif
@@ -87,11 +92,14 @@ struct LdsX {
     f4v stg[C * 17];                   // Doppler staging [chirp][34 c2]: 32 bins + 2 pad (conflict-free both ways)
     c2 rt[NW][1216];                   // per-wave transposes: range 8 x 136 and 64 x 18, Doppler 4 x 304
   } u;
-  c2 twr1[14][64];
-  c2 twr2[15][64];
-  c2 twd1[15][64];
-  float wdl[16][64];                   // 2chebwin of chirp (l & 15) + 16 i
-  f4v cwp[16][64];                     // {cal w', w'} of sample 2 l + e + 128 i, index 2 i + e (w' = IF_scale 2blackman)
+  // per-lane constants packed so that every read is one ds_read_b128 (4 LDS cycles per wave;
+  // a c2 table read by pairs became ds_read2_b64 at 8 cycles, the {cal w', w'} table ds_read_b96 at 8)
+  f4v tw1[7][64];                      // {W1024^((2l) k1), W1024^((2l + 1) k1)}, k1 = 1..7
+  f4v tw2[8][64];                      // {W128^(a0 s1), W128^(a0 (s1 + 1))}, s1 = 1, 3, .., 15 (a0 = l & 7)
+  f4v twd[8][64];                      // {W256^(q d0), W256^(q (d0 + 1))}, d0 = 1, 3, .., 15 (q = l & 15)
+  f4v wdl[4][64];                      // 2chebwin of chirps (l & 15) + 16 i, i = 4 g .. 4 g + 3
+  f4v wq[4][64];                       // w' = IF_scale 2blackman of samples 2 l + e + 128 i, index v = 2 i + e = 4 g .. 4 g + 3
+  c2 cwq[16][64];                      // cal w' of the same samples (read by the reference-chirp wave only)
   float key[GP];                       // candidate key per group position (profile or -1)
 #ifndef XK_NOREF
   f4v x0[512];                         // the frame's reference chirp (chirp 0) as loaded, c64 pairs (fp16: widened)
@@ -195,8 +203,12 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 
   using TP = std::conditional_t<H, h4v, f4v>;
   const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
-  // hand-off slot element: c64, or c32h holding X / Nr (exact power of two) for fp16 storage
-  constexpr int kES = H ? 4 : 8, kGL = H ? 4 : 8;     // bytes per slot element, group loads per thread
+  // hand-off slot element: c64 in both storage modes.  (c32h slots holding X / Nr under fp16
+  // storage, XK_SLOT16, run 3.67 vs 4.1 ms per 4096 frames, but the slow-time rows are then
+  // |X| of fp16-rounded values: 4.5e-4 relative, 0.15 dB in the spectrogram against the
+  // 0.05 dB bar of SURVEY 8d, measured at 4096 frames by bench.py's full-size check.)
+  constexpr bool S16 = H && kSlot16;
+  constexpr int kES = S16 ? 4 : 8, kGL = S16 ? 4 : 8;     // bytes per slot element, group loads per thread
   constexpr int64_t kSlotBytes = (int64_t)NK * C * GP * kES;
   constexpr float kXS = 1.0f / NR, kXU = (float)NR;
 #ifndef XK_NOREF
@@ -221,16 +233,20 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
   for (int i = tid; i < 44 * 64; i += 512) {
     const c2 v = tov(a.xtab[i]);
-    if (i < XT_R2) L.twr1[i >> 6][i & 63] = v;
-    else if (i < XT_D1) L.twr2[(i - XT_R2) >> 6][i & 63] = v;
-    else L.twd1[(i - XT_D1) >> 6][i & 63] = v;
+    const int l = i & 63;
+    c2* d;
+    if (i < XT_R2) { const int t = i >> 6; d = reinterpret_cast<c2*>(&L.tw1[t >> 1][l]) + (t & 1); }
+    else if (i < XT_D1) { const int t = (i - XT_R2) >> 6; d = reinterpret_cast<c2*>(&L.tw2[t >> 1][l]) + (t & 1); }
+    else { const int t = (i - XT_D1) >> 6; d = reinterpret_cast<c2*>(&L.twd[t >> 1][l]) + (t & 1); }
+    *d = v;
   }
-  for (int i = tid; i < 16 * 64; i += 512) L.wdl[i >> 6][i & 63] = a.wd[(i & 15) + 16 * (i >> 6)];
+  for (int i = tid; i < 16 * 64; i += 512) reinterpret_cast<float*>(&L.wdl[i >> 8][i & 63])[(i >> 6) & 3] = a.wd[(i & 15) + 16 * (i >> 6)];
   // :203-205 per-lane constants of samples n = 2 lane + e + 128 i: w' = IF_scale 2blackman, cal w'
   for (int i = tid; i < 16 * 64; i += 512) {
     const int l = i & 63, v = i >> 6, n = 2 * l + (v & 1) + 128 * (v >> 1);
     const float4 cv = n < S ? a.calw[n] : make_float4(0.f, 0.f, 0.f, 0.f);
-    L.cwp[v][l] = f4v{cv.x * cv.z, cv.y * cv.z, cv.z, 0.f};
+    reinterpret_cast<float*>(&L.wq[v >> 2][l])[v & 3] = cv.z;
+    L.cwq[v][l] = c2{cv.x * cv.z, cv.y * cv.z};
   }
   const c2 csum = c2{a.cal_sum.x, a.cal_sum.y};
   const float invS = 1.0f / (float)S;
@@ -241,8 +257,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #ifdef XK_PRIO     // A/B: static priority for the second-dispatched half of the waves (MI355X_MICROARCH item 4)
   if (w >= 4) __builtin_amdgcn_s_setprio(1);
 #endif
-#ifdef XK_STAMPS   // diagnostic build: per-phase time of block 0..255's steps (100 MHz clock)
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_t = __builtin_amdgcn_s_memrealtime();
+#ifdef XK_STAMPS   // diagnostic build: per-phase time of every block's steps, waves 0 and 4 (100 MHz clock)
+  constexpr int NST = 10;
+  unsigned long long st_acc[NST] = {}, st_t = __builtin_amdgcn_s_memrealtime();
+  const unsigned long long st_c0 = __builtin_amdgcn_s_memtime(), st_r0 = st_t;   // shader clock vs 100 MHz
   auto stamp = [&](int i) {
     const unsigned long long n = __builtin_amdgcn_s_memrealtime();
     st_acc[i] += n - st_t;
@@ -263,14 +281,14 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     }
   };
 
-  // ---------------- R: one chirp per wave (:203-205) ----------------
+  // ---------------- R: one chirp per wave (:203-205), in pieces ----------------
 #ifndef XK_NOREF
   const bool refw = k == 0 && w == 0;                   // chirp 0: the frame's reference, transformed as it is
   const float dsc = refw ? 0.f : 1.f;                   // other chirps: x - x_0 (cal cancels)
   const c2 csum_w = refw ? csum : c2{0.f, 0.f};
-  const float calk = refw ? 1.f : 0.f;
 #endif
-  auto range = [&](const TP (&xin)[8], char* __restrict__ slot) __attribute__((always_inline)) {
+  // R1: conditioning, DFT8 over i of both a = 2 lane + e, twiddle W1024^(a k1)
+  auto r_prep = [&](const TP (&xin)[8], c2 (&z0)[8], c2 (&z1)[8]) __attribute__((always_inline)) {
     c2 v[16];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -288,65 +306,75 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     c2 sm = (v[0] + v[1]) + (v[2] + v[3]);
 #pragma unroll
     for (int n = 4; n < 16; n += 4) sm += (v[n] + v[n + 1]) + (v[n + 2] + v[n + 3]);
+    float wv[16];
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f4v t = L.wq[g][lane];
+      wv[4 * g] = t.x; wv[4 * g + 1] = t.y; wv[4 * g + 2] = t.z; wv[4 * g + 3] = t.w;
+    }
 #ifndef XK_NOREF
     const c2 mu = (wave_sum_c(sm) - csum_w) * invS;     // :204 mean of (x - cal), or of x - x_0, over the chirp
+    // (d - mu_d) w' for the chirps taken against the reference (cal cancels); the reference
+    // chirp's wave (uniform branch) also subtracts cal w': (x - cal - mu) w'
+    if (refw) {
 #pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      const f4v cp = L.cwp[n][lane];
-      v[n] = __builtin_elementwise_fma(v[n] - mu, cp.zz, -(cp.xy * calk));   // (x - cal - mu) w' / (d - mu_d) w'
+      for (int n = 0; n < 16; ++n) v[n] = __builtin_elementwise_fma(v[n] - mu, c2{wv[n], wv[n]}, -L.cwq[n][lane]);
+    } else {
+#pragma unroll
+      for (int n = 0; n < 16; ++n) v[n] = (v[n] - mu) * wv[n];
     }
 #else
     const c2 mu = (wave_sum_c(sm) - csum) * invS;       // :204 mean of (x - cal) over the chirp
 #pragma unroll
-    for (int n = 0; n < 16; ++n) {
-      const f4v cp = L.cwp[n][lane];
-      v[n] = __builtin_elementwise_fma(v[n] - mu, cp.zz, -cp.xy);   // (x - cal - mu) w'
-    }
+    for (int n = 0; n < 16; ++n) v[n] = __builtin_elementwise_fma(v[n] - mu, c2{wv[n], wv[n]}, -L.cwq[n][lane]);
 #endif
-    c2 z0[8], z1[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { z0[i] = v[2 * i]; z1[i] = v[2 * i + 1]; }
     dft8p(z0);
     dft8p(z1);
 #pragma unroll
     for (int k1 = 1; k1 < 8; ++k1) {
-      z0[k1] = cmul_a(z0[k1], L.twr1[2 * (k1 - 1)][lane]);
-      z1[k1] = cmul_a(z1[k1], L.twr1[2 * (k1 - 1) + 1][lane]);
+      const f4v t = L.tw1[k1 - 1][lane];
+      z0[k1] = cmul_a(z0[k1], t.xy);
+      z1[k1] = cmul_a(z1[k1], t.zw);
     }
-    c2* rt = L.u.rt[w];
-#pragma unroll
-    for (int k1 = 0; k1 < 8; ++k1)
-      *reinterpret_cast<f4v*>(&rt[k1 * 136 + 2 * lane]) = f4v{z0[k1].x, z0[k1].y, z1[k1].x, z1[k1].y};
-    cfence();
-    const int k1 = lane >> 3, a0 = lane & 7;
-    c2 u[16];
-#pragma unroll
-    for (int a1 = 0; a1 < 16; ++a1) u[a1] = rt[k1 * 136 + a0 + 8 * a1];
-    cfence();
+  };
+  c2* const rt = L.u.rt[w];                             // this wave's transpose region (range T1, T2; Doppler TD)
+  const int k1 = lane >> 3, a0 = lane & 7, hh = lane & 7;
+  // R2: DFT16 over a1 (lane 8 k1 + a0), twiddle W128^(a0 s1)
+  auto r_mid = [&](c2 (&u)[16]) __attribute__((always_inline)) {
     dft16p<1>(u);
 #pragma unroll
-    for (int s1 = 1; s1 < 16; ++s1) u[s1] = cmul_a(u[s1], L.twr2[s1 - 1][lane]);
+    for (int s1 = 1; s1 < 16; s1 += 2) {
+      const f4v t = L.tw2[s1 >> 1][lane];
+      u[s1] = cmul_a(u[s1], t.xy);
+      if (s1 < 15) u[s1 + 1] = cmul_a(u[s1 + 1], t.zw);
+    }
+  };
+  auto r_t2 = [&](const c2 (&u)[16], c2 (&q0)[8], c2 (&q1)[8]) __attribute__((always_inline)) {
 #pragma unroll
     for (int h = 0; h < 8; ++h)
       *reinterpret_cast<f4v*>(&rt[lane * 18 + 2 * h]) = f4v{u[2 * h].x, u[2 * h].y, u[2 * h + 1].x, u[2 * h + 1].y};
     cfence();
-    const int hh = lane & 7;
-    c2 q0[8], q1[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const f4v t = *reinterpret_cast<const f4v*>(&rt[(k1 * 8 + j) * 18 + 2 * hh]);
-      q0[j] = t.xy;
-      q1[j] = t.zw;
+    for (int jj = 0; jj < 8; ++jj) {
+      const f4v t = *reinterpret_cast<const f4v*>(&rt[(k1 * 8 + jj) * 18 + 2 * hh]);
+      q0[jj] = t.xy;
+      q1[jj] = t.zw;
     }
     cfence();
+  };
+  // R3: DFT8 over a0 and the slot stores
+  auto r_end = [&](c2 (&q0)[8], c2 (&q1)[8], char* __restrict__ slot) __attribute__((always_inline)) {
     dft8p(q0);
     dft8p(q1);
     // bins k1 + 16 hh + 8 e + 128 s2 -> group 4 s2 + 2 e + (k1 >> 2), position lane & 31
     const int c = k * NW + w;
-    // slot stores are buffer stores (and the only ones in k_rdx): tools/check_vmcnt.py finds them
-    // by that to prove, on the built code, that every publish waits for them
+    // slot stores are buffer stores without a cache-policy flag (the only such stores in k_rdx):
+    // tools/check_vmcnt.py finds them by that to prove, on the built code, that every publish
+    // waits for them
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, kSlotBytes, 0x00020000);
-    if constexpr (H) {   // fp16 storage: the slot holds X / Nr as c32h (half the bytes of the hand-off)
+    if constexpr (S16) {   // XK_SLOT16: the slot holds X / Nr as c32h (half the bytes of the hand-off)
       const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 4;
 #pragma unroll
       for (int s2 = 0; s2 < 8; ++s2) {
@@ -355,20 +383,20 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h0), rs, o + 4 * s2 * C * GP * 4, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h1), rs, o + (4 * s2 + 2) * C * GP * 4, 0, 0);
       }
-      return;
-    }
-    const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 8;
+    } else {
+      const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 8;
 #pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2) {
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q0[s2]), rs, o + 4 * s2 * C * GP * 8, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q1[s2]), rs, o + (4 * s2 + 2) * C * GP * 8, 0, 0);
+      for (int s2 = 0; s2 < 8; ++s2) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q0[s2]), rs, o + 4 * s2 * C * GP * 8, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q1[s2]), rs, o + (4 * s2 + 2) * C * GP * 8, 0, 0);
+      }
     }
   };
 
-  // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259) ----------------
+  // ---------------- D: the 32 bins of group k (:210, :216-219, :257-259), in pieces ----------------
   // buffer_load ... sc1: the CU's L1 is bypassed (no stale lines from the slot's
   // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
-  // (fp16 storage: the group is 32 KiB of c32h, 4 loads per thread, widened and scaled back by Nr
+  // (XK_SLOT16: the group is 32 KiB of c32h, 4 loads per thread, widened and scaled back by Nr
   // into the same fp32 staging image)
   auto ld_group = [&](const char* __restrict__ grp, f4v (&t)[8]) __attribute__((always_inline)) {
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(grp), (short)0, C * GP * kES, 0x00020000);
@@ -376,7 +404,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     for (int i = 0; i < kGL; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
   };
   auto stage = [&](const f4v (&t)[8]) __attribute__((always_inline)) {
-    if constexpr (H) {
+    if constexpr (S16) {
 #pragma unroll
       for (int i = 0; i < kGL; ++i) {
         const int e = tid + 512 * i;            // 16-byte piece: chirp e >> 3, positions 4 (e & 7) .. + 3
@@ -394,11 +422,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       }
     }
   };
-  // D of one frame from its staged group (the caller staged it and synchronised)
-  auto doppler_staged = [&](int64_t f) __attribute__((always_inline)) {
-    const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
-    const int r = xcd_bin(k, p);
-    c2 xv[16];
+  const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
+  const int r = xcd_bin(k, p);
+  // D1: the rows from the staged group, :217 row mean, :210 / :265 row max |X| -> profile, candidate keys
+  auto d_rows = [&](int64_t f, c2 (&xv)[16], c2& x0r, c2& mu) __attribute__((always_inline)) {
     {
       const c2* stg = reinterpret_cast<const c2*>(L.u.stg);
 #pragma unroll
@@ -406,8 +433,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     }
 #ifndef XK_NOREF
     // the slot holds X_0 for chirp 0 and X'_k = X_k - X_0 for the others (reference chirp above)
-    const c2 x0r = reinterpret_cast<const c2*>(L.u.stg)[p];   // X_0 of this row (chirp 0: q = 0, i = 0)
-    if (q == 0) xv[0] = c2{0.f, 0.f};                           // X'_0 = 0
+    x0r = reinterpret_cast<const c2*>(L.u.stg)[p];       // X_0 of this row (chirp 0: q = 0, i = 0)
+    if (q == 0) xv[0] = c2{0.f, 0.f};                     // X'_0 = 0
     // :210 / :265 row max |X| over the 256 chirps, X_k = X'_k + X_0
     float pm = fmaxf(fmaxf(abs2v(xv[0] + x0r), abs2v(xv[1] + x0r)), fmaxf(abs2v(xv[2] + x0r), abs2v(xv[3] + x0r)));
 #pragma unroll
@@ -419,8 +446,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #pragma unroll
     for (int i = 4; i < 16; i += 4) sm += (xv[i] + xv[i + 1]) + (xv[i + 2] + xv[i + 3]);
 #else
-    const c2 x0r = c2{0.f, 0.f};
-    // :217 row mean and :210 / :265 row max |X| over the 256 chirps
+    x0r = c2{0.f, 0.f};
     c2 sm = (xv[0] + xv[1]) + (xv[2] + xv[3]);
     float pm = fmaxf(fmaxf(abs2v(xv[0]), abs2v(xv[1])), fmaxf(abs2v(xv[2]), abs2v(xv[3])));
 #pragma unroll
@@ -431,40 +457,53 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
     sm = c2{row_sum16(sm.x), row_sum16(sm.y)};
     pm = __int_as_float(row_max16(__float_as_int(pm)));
-    const c2 mu = sm * (1.0f / (float)C);
+    mu = sm * (1.0f / (float)C);
     const float pr = sqrtf(pm);
     a.profile[f * NR + r] = pr;        // all 16 lanes of the row (same value): a store on every path
     if (q == 0) {
       const double rng = (double)r * a.dist_per_bin;
       L.key[p] = (r >= 1 && r <= NR - 2 && rng >= a.min_d && rng <= a.max_d && pr > a.range_thr) ? pr : -1.f;
     }
-    __syncthreads();                   // keys of all 32 rows in; staging read out (the transposes reuse it)
-    stamp(3);
-    {   // slow-time candidates (:257-259): the XCD_CAND strongest in-window rows of the group
-      float kv = lane < GP ? L.key[lane] : -1.f;
-      const int ki = xcd_bin(k, lane & (GP - 1));
+  };
+  // D2 (after the keys barrier): slow-time candidates (:257-259), the XCD_CAND strongest
+  // in-window rows of the group
+  auto d_cand = [&](int64_t f, const c2 (&xv)[16], c2 x0r) __attribute__((always_inline)) {
+    float kv = lane < GP ? L.key[lane] : -1.f;
+    const int ki = xcd_bin(k, lane & (GP - 1));
 #pragma unroll
-      for (int c = 0; c < XCD_CAND; ++c) {
-        float bv = kv;
-        int bi = ki;
-        wave_argmax_dpp(bv, bi);                               // same in every wave: ties -> lowest bin
-        const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
-        if (w == 0 && lane == 0) a.cand_idx[(f * XCD_TILES + k) * XCD_CAND + c] = sel;
-        if (sel >= 0 && r == sel) {
-          float* __restrict__ row = a.cand_rows + ((f * XCD_TILES + k) * XCD_CAND + c) * (int64_t)C;
+    for (int c = 0; c < XCD_CAND; ++c) {
+      float bv = kv;
+      int bi = ki;
+      wave_argmax_dpp(bv, bi);                               // same in every wave: ties -> lowest bin
+      const int sel = (bv < 0.f || a.force_fix) ? -1 : bi;
+      if (w == 0 && lane == 0) a.cand_idx[(f * XCD_TILES + k) * XCD_CAND + c] = sel;
+      if (sel >= 0 && r == sel) {
+        float* __restrict__ row = a.cand_rows + ((f * XCD_TILES + k) * XCD_CAND + c) * (int64_t)C;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) row[q + 16 * i] = abs2v(xv[i] + x0r);
-        }
-        if (ki == sel) kv = -1.f;
+        for (int i = 0; i < 16; ++i) row[q + 16 * i] = abs2v(xv[i] + x0r);
       }
+      if (ki == sel) kv = -1.f;
     }
-    // :218 (X - mean) .* 2chebwin, :219 fft over chirps
+  };
+  // D3: :218 (X - mean) .* 2chebwin, :219 DFT16 over i, twiddle W256^(q d0)
+  auto d_a = [&](c2 (&xv)[16], c2 mu) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) xv[i] = (xv[i] - mu) * L.wdl[i][lane];
+    for (int g = 0; g < 4; ++g) {
+      const f4v wv = L.wdl[g][lane];
+      xv[4 * g + 0] = (xv[4 * g + 0] - mu) * wv.x;
+      xv[4 * g + 1] = (xv[4 * g + 1] - mu) * wv.y;
+      xv[4 * g + 2] = (xv[4 * g + 2] - mu) * wv.z;
+      xv[4 * g + 3] = (xv[4 * g + 3] - mu) * wv.w;
+    }
     dft16p<1>(xv);
 #pragma unroll
-    for (int d0 = 1; d0 < 16; ++d0) xv[d0] = cmul_a(xv[d0], L.twd1[d0 - 1][lane]);
-    c2* rt = L.u.rt[w];
+    for (int d0 = 1; d0 < 16; d0 += 2) {
+      const f4v t = L.twd[d0 >> 1][lane];
+      xv[d0] = cmul_a(xv[d0], t.xy);
+      if (d0 < 15) xv[d0 + 1] = cmul_a(xv[d0 + 1], t.zw);
+    }
+  };
+  auto d_td = [&](c2 (&xv)[16]) __attribute__((always_inline)) {
 #pragma unroll
     for (int h = 0; h < 8; ++h)
       *reinterpret_cast<f4v*>(&rt[304 * pp + 18 * q + 2 * h]) = f4v{xv[2 * h].x, xv[2 * h].y, xv[2 * h + 1].x, xv[2 * h + 1].y};
@@ -472,9 +511,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #pragma unroll
     for (int m0 = 0; m0 < 16; ++m0) xv[m0] = rt[304 * pp + 18 * m0 + q];
     cfence();
-    dft16p<1>(xv);                     // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
-    stamp(4);
-    // :219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)]
+  };
+  // D4: the RD row stores (:219 fftshift(., 2): position q + 16 d1s holds D[q + 16 ((d1s + 8) mod 16)])
+  // or, without an RD map, the row peak (:233)
+  auto d_store = [&](int64_t f, const c2 (&xv)[16]) __attribute__((always_inline)) {
     if constexpr (RD) {
       // RD rows: buffer stores with the sc1 cache policy (the written lines stream out of the
       // XCD's L2 instead of evicting the hand-off slots; measured 4.93 -> 4.67 ms per 4096
@@ -509,87 +549,117 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   char* __restrict__ slots0 = reinterpret_cast<char*>(a.xcube) + (int64_t)x * NS * kSlotBytes;
   auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % NS) * kSlotBytes; };
   auto frame = [&](int j) __attribute__((always_inline)) { return x + (int64_t)T * j; };
-  // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - NS,
-  // and R(j) runs after this member saw ready(j - 2); a member publishes R(j - 2)
-  // only after its own reads of frame j - 4 (at most) have returned, so slots >= 4.
   TP xin[8];
+  f4v grp[8];
   if (nj > 0) ld_chirp(frame(0), xin);
-  // Step j: R(j - 1) is published first, its slot stores having drained under
-  // D(j - 3): the wait counts the vector-memory operations every path issues
-  // after them (the next frame's reference and chirp loads, the profile store,
-  // the RD stores), which tools/check_vmcnt.py proves on the built code.  Then
-  // the group of frame j - 2 is loaded, R(j) runs while it lands, the group is
-  // staged once it is in (vmcnt(16): only R(j)'s slot stores behind it), the
-  // next chirp's loads go out and D(j - 2) runs.  Steps 0-2 and the last two
-  // are peeled and every flag is a compile-time constant, so each copy is
-  // straight-line code with a static wait count; the next frame's loads are
-  // unconditional (the last steady step reloads the last frame).
-  constexpr int kLd = 8 + (XK_REF ? 1 : 0);              // next frame's chirp (+ reference) loads
-  constexpr int kD = 1 + (RD ? XK_RD_STORES : 1);         // D's unconditional stores: profile + RD rows / row peaks
+  // Step j runs R(j) and D(j - 3) side by side in every wave, so that the range FFT's and the
+  // Doppler FFT's dependency chains (DPP sums, LDS transposes) cover each other:
+  //   B1 (frame j's reference chirp into LDS; wave 0 polls ready(j - 2) meanwhile)
+  //   staging of group j - 3 (loaded in step j - 1) -> B2 -> rows, profile, keys
+  //   -> publish R(j - 1) (its slot stores waited for) -> B3 -> group loads of frame j - 2
+  //   -> candidates -> R1 | D3 -> TD -> T1 | D DFT16 -> R2 -> T2 -> R3 + slot stores
+  //   -> RD stores, next frame's loads (issued as soon as R1 freed the registers).
+  // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - 4 and runs after
+  // this member saw ready(j - 2); a member publishes R(j - 2) only after its group loads of
+  // frame j - 4, issued before R(j - 2)'s slot stores, have returned (vmcnt is in order).
+  // The publish wait counts what every path issues after the slot stores: D(j - 4)'s RD stores
+  // (or row peaks) and the profile store of D(j - 3); tools/check_vmcnt.py proves it on the
+  // built code.  Steps 0-3 and the last three are peeled, every flag a compile-time constant.
+  constexpr int kRDs = RD ? XK_RD_STORES : 1;                  // D's stores after the slot stores
   // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
-  auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto NEXT) __attribute__((always_inline)) {
-    const bool dj = DJ, rj = RJ, pub = PUB, next = NEXT;
-    f4v grp[8];
-    // one barrier for both: after it every wave's slot stores of R(j - 1) are in the
-    // L2 (publish) and tid 0 has seen every member's R(j - 2) (the group may be read)
-    if (pub) vm_wait<decltype(CNT)::value>();
-    if (dj)   // wave 0 polls (scalar: its vector memory operations stay in flight); the barrier releases the rest
-      if (w == 0) wait_ge(&ready[((j - 2) % NS) * 32], (unsigned)(NK * ((j - 2) / NS + 1)), a.xctr + XCD_ABORT, a.xerr);
+  auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT) __attribute__((always_inline)) {
+    const bool dj = DJ, rj = RJ, pub = PUB, gj = GJ, next = NEXT;
+    const int64_t fd = frame(j - 3);
+    if (j >= 1) __syncthreads();       // B1: step j - 1 done in every wave (transpose regions, keys, x0)
+    stamp(0);
 #ifndef XK_NOREF
     if (rj)
-      if (j >= 1) put_ref();           // frame j's reference chirp (R(j - 1) is done with the last one)
+      if (j >= 1) put_ref();           // frame j's reference chirp (read by R1 after B3)
 #endif
-    if (pub || dj) __syncthreads();
+    if (gj)   // wave 0 polls (scalar: its vector memory operations stay in flight); B2 releases the rest
+      if (w == 0) wait_ge(&ready[((j - 2) % NS) * 32], (unsigned)(NK * ((j - 2) / NS + 1)), a.xctr + XCD_ABORT, a.xerr);
+    if (dj) stage(grp);
+    stamp(1);
+    __syncthreads();                   // B2: staged; x0 of frame j in; ready(j - 2) seen
+    stamp(2);
+    c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
+    if (dj) d_rows(fd, xv, x0r, dmu);
+    stamp(3);
+    if (pub) vm_wait<decltype(CNT)::value>();   // R(j - 1)'s slot stores are in the L2
+    if (dj || pub) __syncthreads();    // B3: keys in, staging read out; every wave's R(j - 1) stores done
     // the publish: wave 0 adds 1 to the slot's ready counter; every other wave adds 0 to a word
     // of its own, so that every wave issues the same vector-memory operations and the compiler's
-    // vmcnt waits behind them never wait for an atomic (a wave-0-only atomic made wave 0 wait
-    // for its return in R(j): the merged paths count it as possibly outstanding)
+    // vmcnt waits behind them never wait for an atomic
     if (pub)
       if (lane == 0)
         __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % NS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
                                w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (dj) ld_group(slot(j - 2) + (int64_t)k * C * GP * kES, grp);
+    stamp(4);
+    if (gj) ld_group(slot(j - 2) + (int64_t)k * C * GP * kES, grp);
+    if (dj) d_cand(fd, xv, x0r);
     stamp(5);
-    if (rj) range(xin, slot(j));
-    stamp(0);
-    if (rj) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // the group is in (R(j)'s slot stores may not be)
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();                   // the range transposes are free for the staging
-    if (dj) stage(grp);
-    cfence();
-    if (next) {                        // in flight during D(j - 2)
+    c2 z0[8], z1[8], u[16];
+    if (rj) r_prep(xin, z0, z1);
+    if (next) {                        // R1 freed the chirp registers: the next frame's loads go out
       const int jn = j + 1 < nj ? j + 1 : nj - 1;
 #ifndef XK_NOREF
       ld_ref(frame(jn));
 #endif
       ld_chirp(frame(jn), xin);
     }
-    stamp(1);
-    if (dj) {
-      __syncthreads();                 // staged
-      stamp(2);
-      doppler_staged(frame(j - 2));
+    if (dj) d_a(xv, dmu);
+    stamp(6);
+    if (dj) d_td(xv);
+    if (rj) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        *reinterpret_cast<f4v*>(&rt[kk * 136 + 2 * lane]) = f4v{z0[kk].x, z0[kk].y, z1[kk].x, z1[kk].y};
+      cfence();
     }
+    if (dj) dft16p<1>(xv);             // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
+    if (rj) {
+#pragma unroll
+      for (int a1 = 0; a1 < 16; ++a1) u[a1] = rt[k1 * 136 + a0 + 8 * a1];
+      cfence();
+    }
+    stamp(7);
+    if (rj) {
+      c2 q0[8], q1[8];
+      r_mid(u);
+      r_t2(u, q0, q1);
+      r_end(q0, q1, slot(j));
+    }
+    stamp(8);
+    if (dj) d_store(fd, xv);
+    stamp(9);
   };
   using T_ = std::true_type;
   using F_ = std::false_type;
-  if (nj >= 3) {
-    body(0, F_{}, T_{}, F_{}, std::integral_constant<int, 0>{}, T_{});
-    body(1, F_{}, T_{}, T_{}, std::integral_constant<int, kLd>{}, T_{});
-    body(2, T_{}, T_{}, T_{}, std::integral_constant<int, kLd>{}, T_{});
-    for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, std::integral_constant<int, kLd + kD>{}, T_{});
-    body(nj, T_{}, F_{}, T_{}, std::integral_constant<int, kLd + kD>{}, F_{});
-    body(nj + 1, T_{}, F_{}, F_{}, std::integral_constant<int, 0>{}, F_{});
+  using C0 = std::integral_constant<int, 0>;
+  using CF = std::integral_constant<int, kRDs + 1>;
+  if (nj >= 4) {
+    //   j       DJ   RJ   PUB  CNT                GJ   NEXT
+    body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{});
+    body(1,      F_{}, T_{}, T_{}, C0{},                          F_{}, T_{});
+    body(2,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{});
+    body(3,      T_{}, T_{}, T_{}, std::integral_constant<int, 1>{}, T_{}, T_{});
+    for (int j = 4; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{});
+    body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{});
+    body(nj + 1, T_{}, F_{}, F_{}, C0{},                          T_{}, F_{});
+    body(nj + 2, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{});
   } else {
-    // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
+    // 1-3 frames on this XCD (launches of < 32 frames): one copy with run-time flags, every
     // publish waiting for everything
-    for (int j = 0; j < nj + 2; ++j)
-      body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj, std::integral_constant<int, 0>{}, j + 1 < nj);
+    for (int j = 0; j < nj + 3; ++j)
+      body(j, j >= 3, j < nj, j >= 1 && j - 1 < nj, C0{}, j >= 2 && j - 2 < nj, j + 1 < nj);
   }
 #ifdef XK_STAMPS
-  if (tid == 0) {
-    for (int i = 0; i < 6; ++i) a.dbg[(int64_t)blockIdx.x * 8 + i] = st_acc[i];
-    a.dbg[(int64_t)blockIdx.x * 8 + 6] = (unsigned long long)nj;
+  if (lane == 0 && (w == 0 || w == 4)) {
+    unsigned long long* d = a.dbg + ((int64_t)blockIdx.x * 2 + (w >> 2)) * 16;
+    for (int i = 0; i < NST; ++i) d[i] = st_acc[i];
+    d[13] = __builtin_amdgcn_s_memtime() - st_c0;
+    d[14] = __builtin_amdgcn_s_memrealtime() - st_r0;
+    d[15] = (unsigned long long)nj;
   }
 #endif
 }

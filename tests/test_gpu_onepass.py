@@ -191,9 +191,9 @@ def test_onepass_fp16_storage(onepass, monkeypatch, F, nts, fix):
     x = iq16.astype(np.float32).view(np.complex64)[..., 0]
     ref = O.process_frames(x, cal, p, wr, wd, want_cube=True, want_rd=True, rd_all_rows=True)
     assert rd_rel_err(got["rd"], ref["rd"], ref["cube"], wd, 256).max() <= TOL_FP16_REL_L2
-    # profile and slow rows: the fp16-storage bar (the XCD schedule hands the range cube over
-    # as c32h; the 8-tile single pass keeps it in fp32 registers); detections exact except
-    # frames whose two strongest bins are within fp16 rounding of each other
+    # profile and slow rows: fp32 arithmetic on fp16-exact inputs (the range cube is handed
+    # over as c64 under fp16 storage too), checked at the fp16-storage bar; detections exact
+    # except frames whose two strongest bins are within fp16 rounding of each other
     assert rel_l2(got["profile"], ref["profile"], axis=1).max() <= TOL_FP16_REL_L2
     ok = ~near_tie_frames(ref["profile"], rtol=1e-3)
     for k in ("tgt_count", "tgt_range_idx", "tgt_doppler_idx"):

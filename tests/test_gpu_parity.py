@@ -167,11 +167,15 @@ def test_synth_generator_matches_oracle(engine):
 
 
 def test_fp16_storage_tolerance(engine):
-    """Config 4 fp16 storage: fp16 IQ in, fp16 RD out, fp32 arithmetic."""
+    """Config 4 fp16 storage: fp16 IQ in, fp16 RD out, fp32 arithmetic.  The slow-time rows
+    come from fp32 arithmetic on the fp16-exact inputs, so they meet the fp32 bar: fp16
+    hand-off slots (XK_SLOT16) put them at 4.5e-4 and the spectrogram at 0.15 dB over the
+    4096 frames of bench.py's full-size check, which the 3 frames this test ran before did
+    not show (0.05 dB bar)."""
     import torch
     cfg, p, wr, wd, cal = case(1024, 256, 1024, 256, P.THROUGHPUT)
     engine.set_taps(cfg, cal, wr, wd)
-    F = 3
+    F = 32
     iq = O.synth_frames(F, 256, 1024, 1024, 256, p["dist_per_bin"])
     iq16 = np.stack([iq.real, iq.imag], -1).astype(np.float16)
     d_iq = torch.from_numpy(iq16).cuda()
@@ -195,6 +199,7 @@ def test_fp16_storage_tolerance(engine):
     # the STFT of the fp16-path slow-time rows (config 4: Hann(20), hop 1, nfft 64):
     # fp16 storage bar |dB error| <= TOL_FP16_DB where psd > -60 dB
     has = ref["tgt_count"] > 0
+    assert rel_l2(outs["slow_mag"].cpu().numpy()[has], ref["slow_mag"][has], axis=1).max() <= TOL_FP32_REL_L2
     x = outs["slow_mag"].cpu().numpy()[has].reshape(-1).astype(np.float64)
     xr = ref["slow_mag"][has].reshape(-1)
     got = engine.stft(x, O.stft_window("hann"), 19, 1 / p["prt"], nfft=64, n_log_bins=0)

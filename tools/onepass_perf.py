@@ -33,6 +33,8 @@ def main(F=4096, reps=10, which="streams,onepass"):
                 tgt_doppler_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
                 slow_mag=torch.empty((F, cfg.pn), device=dev))
     d_rd = torch.empty((F, cfg.nr, cfg.nd, 2), dtype=tdt, device=dev)
+    if os.environ.get("NORD", "0") == "1":      # no RD map (row peaks only): the RD stores' share of the time
+        d_rd = None
     es = 4 if fp16 else 8
     byt = F * (cfg.pn * cfg.nts * es + cfg.nr * cfg.nd * es + cfg.nr * 4 + cfg.pn * 4)
     modes = {"streams": FMCW_PIPE_STREAMS, "onepass": FMCW_PIPE_ONEPASS, "xcd": FMCW_PIPE_XCD}
