@@ -69,7 +69,6 @@ using namespace op;
 #else
 #define XK_REF 1
 #endif
-#define XK_RD_STORES 16                // RD stores per lane and row group
 #ifdef XK_SLOT16
 constexpr bool kSlot16 = true;         // A/B only: fp16 hand-off slots under fp16 storage (fails the STFT bar, below)
 #else
@@ -166,6 +165,15 @@ __device__ __forceinline__ int row_min16(int v) {
   v = min(v, dppi<0x4E>(v));
   v = min(v, dppi<0x141>(v));
   return min(v, dppi<0x140>(v));
+}
+
+// Lanes 2m, 2m + 1 hold columns p, p + 1 of two rows A and B (one value each): afterwards the
+// even lane holds both columns of row A, the odd lane both columns of row B, ready for one
+// double-width store at column p (even) / p - 1 (odd) of its row.  One DPP swap per dword.
+__device__ __forceinline__ f4v pair_cols(c2 A, c2 B, bool odd) {
+  const c2 snd = odd ? A : B;
+  const c2 rcv = c2{dppf<0xB1>(snd.x), dppf<0xB1>(snd.y)};
+  return odd ? f4v{rcv.x, rcv.y, B.x, B.y} : f4v{A.x, A.y, rcv.x, rcv.y};
 }
 
 }  // namespace xk
@@ -385,11 +393,14 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       }
     } else {
       const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 8;
+      // 16-byte stores (cdna_hip_programming.md T21: a store tail is issue-bound per instruction;
+      // 4.69 -> 4.63 ms per 4096 frames against 16 8-byte stores): lane pairs swap one value, the
+      // even lane stores both columns of the e = 0 row, the odd lane both of the e = 1 row
+      const bool odd = lane & 1;
+      const int ow = odd ? o - 8 + 2 * C * GP * 8 : o;
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q0[s2]), rs, o + 4 * s2 * C * GP * 8, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2v, q1[s2]), rs, o + (4 * s2 + 2) * C * GP * 8, 0, 0);
-      }
+      for (int s2 = 0; s2 < 8; ++s2)
+        __builtin_amdgcn_raw_buffer_store_b128(pair_cols(q0[s2], q1[s2], odd), rs, ow + 4 * s2 * C * GP * 8, 0, 0);
     }
   };
 
@@ -565,7 +576,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // The publish wait counts what every path issues after the slot stores: D(j - 4)'s RD stores
   // (or row peaks) and the profile store of D(j - 3); tools/check_vmcnt.py proves it on the
   // built code.  Steps 0-3 and the last three are peeled, every flag a compile-time constant.
-  constexpr int kRDs = RD ? XK_RD_STORES : 1;                  // D's stores after the slot stores
+  constexpr int kRDs = RD ? 16 : 1;                             // D's stores after the slot stores (RD rows / row peak)
   // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
   auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT) __attribute__((always_inline)) {
     const bool dj = DJ, rj = RJ, pub = PUB, gj = GJ, next = NEXT;

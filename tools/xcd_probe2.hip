@@ -87,7 +87,16 @@ __global__ __launch_bounds__(512, 1) void k_probe(const char* __restrict__ iq, c
       // input is chirp ch = e / 512 (of UC/32), sample pair p = e % 512 -> bins 2p, 2p+1 of group p / 16
       char* s = slots0 + (long)(j % NS) * UB;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(s, (short)0, (int)UB, 0x00020000);
-      if constexpr (W8) {   // k_rdx's shape: 8-byte stores, each half-wave one 256-byte row
+      if constexpr (W8 == 2) {   // k_rdx's exact slot-store shape: wave w = chirp 8k + w, lane = (half, position)
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const int lane = tid & 63, w = tid >> 6, c = k * (UC / 32) + w;   // (UC = 256: one chirp per wave)
+        const int o = (((lane >> 5) * UC + c) * 32 + (lane & 31)) * 8;
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) {
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, xin[s2].xy), rs, o + 4 * s2 * UC * 32 * 8, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, xin[s2].zw), rs, o + (4 * s2 + 2) * UC * 32 * 8, 0, 0);
+        }
+      } else if constexpr (W8) {   // 8-byte stores, each half-wave one 256-byte row
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
           const int e = tid + 512 * i, ch = k * (UC / 32) + (e >> 9), p = e & 511;
@@ -117,7 +126,15 @@ __global__ __launch_bounds__(512, 1) void k_probe(const char* __restrict__ iq, c
         for (int i = 0; i < NL; ++i) grp[i] = grp[i] * 0.998f + u;
       const long f = x + 8L * (j - LAG);
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)k * 32 * UC * 8, (short)0, 32 * UC * 8, 0x00020000);
-      if constexpr (W8) {   // k_rdx's shape: 8-byte sc1 stores, 16 lanes per 128-byte row segment
+      if constexpr (W8 == 2) {   // k_rdx's exact RD shape: wave w rows 4w + pp, lane (pp, q) positions q + 16 d1s
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const int lane = tid & 63, w = tid >> 6, pp = lane >> 4, q = lane & 15, row = 4 * w + pp;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, grp[d].xy), rr, (row * UC + q + 32 * d) * 8, 0, 16);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, grp[d].zw), rr, (row * UC + q + 32 * d + 16) * 8, 0, 16);
+        }
+      } else if constexpr (W8) {   // 8-byte sc1 stores, 16 lanes per 128-byte row segment
         typedef unsigned u2 __attribute__((ext_vector_type(2)));
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
@@ -201,6 +218,8 @@ int main(int argc, char** argv) {
     pr("frame unit, lag 2, 4 slots, 8-B stores", run<256, 2, 0, 0, 1>(iq, cube, rd, ctr, err, F, 4));
     pr("frame unit, lag 2, 4 slots, work", run<256, 2, 24, 16>(iq, cube, rd, ctr, err, F, 4));
     pr("frame unit, lag 2, 4 slots, 8-B stores, work", run<256, 2, 24, 16, 1>(iq, cube, rd, ctr, err, F, 4));
+    pr("frame unit, lag 2, 4 slots, k_rdx store shapes", run<256, 2, 0, 0, 2>(iq, cube, rd, ctr, err, F, 4));
+    pr("frame unit, lag 2, 4 slots, k_rdx store shapes, work", run<256, 2, 24, 16, 2>(iq, cube, rd, ctr, err, F, 4));
   }
   if (which == 0 || which == 2) {
     pr("frame unit, lag 2, 4 slots, work", run<256, 2, 24, 16>(iq, cube, rd, ctr, err, F, 4));
