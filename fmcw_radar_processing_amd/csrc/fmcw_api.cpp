@@ -735,8 +735,8 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
           std::vector<unsigned long long> hh(nblk * 32);
           HIPCHK(hipStreamSynchronize(s));
           HIPCHK(hipMemcpy(hh.data(), a.dbg, hh.size() * 8, hipMemcpyDeviceToHost));
-          static const char* nm[10] = {"B1", "poll+stage", "B2", "rows", "pubwait+B3", "grp+cand", "R1+ld+D3",
-                                       "TD+T1+DFT16", "R2+T2+R3", "RD"};
+          static const char* nm[10] = {"B1", "stage", "B2", "rows", "pubwait+B3", "cand", "R1+ld+D3",
+                                       "poll+grp", "TD..R3", "RD"};
           for (int wv = 0; wv < 2; ++wv) {
             double ph[10] = {}, steps = 0;
             for (int bb = 0; bb < nblk; ++bb) {

@@ -78,6 +78,10 @@ constexpr bool kSlot16 = false;
 #define XK_RD_AUX 16                   // RD store cache policy: sc1 (A/B: 17 = sc0 sc1, 2 = nt)
 #endif
 constexpr int kRdAux = XK_RD_AUX;
+#ifndef XK_NS
+#define XK_NS 2
+#endif
+constexpr int kNS = XK_NS;            // hand-off slots in use per XCD (2..XCD_MAX_SLOTS; see the step loop)
 constexpr int NK = 32;                 // team members (CUs) per XCD
 constexpr int C = 256;                 // chirps = Doppler points
 constexpr int NW = 8;                  // waves per workgroup = chirps per member
@@ -191,7 +195,9 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // stopped, so the XCD is read from HW_REG_XCC_ID and the member index is a
   // ticket drawn on that XCD's counter: 256 blocks give every XCD exactly 32.
   __shared__ int team[2];
+  __shared__ unsigned gflag;           // the last step whose ready(j - 1) wave 0 has seen
   if (tid == 0) {
+    gflag = 0;
     unsigned xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     const int xx = a.xcc_team[xcc & 15];   // the census's team index of this XCC
@@ -558,40 +564,41 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   };
 
   char* __restrict__ slots0 = reinterpret_cast<char*>(a.xcube) + (int64_t)x * NS * kSlotBytes;
-  auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % NS) * kSlotBytes; };
+  auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % kNS) * kSlotBytes; };
   auto frame = [&](int j) __attribute__((always_inline)) { return x + (int64_t)T * j; };
   TP xin[8];
   f4v grp[8];
   if (nj > 0) ld_chirp(frame(0), xin);
-  // Step j runs R(j) and D(j - 3) side by side in every wave, so that the range FFT's and the
+  // Step j runs R(j) and D(j - 2) side by side in every wave, so that the range FFT's and the
   // Doppler FFT's dependency chains (DPP sums, LDS transposes) cover each other:
-  //   B1 (frame j's reference chirp into LDS; wave 0 polls ready(j - 2) meanwhile)
-  //   staging of group j - 3 (loaded in step j - 1) -> B2 -> rows, profile, keys
-  //   -> publish R(j - 1) (its slot stores waited for) -> B3 -> group loads of frame j - 2
-  //   -> candidates -> R1 | D3 -> TD -> T1 | D DFT16 -> R2 -> T2 -> R3 + slot stores
-  //   -> RD stores, next frame's loads (issued as soon as R1 freed the registers).
-  // Slot reuse needs no done counters: R(j) overwrites the slot of frame j - 4 and runs after
-  // this member saw ready(j - 2); a member publishes R(j - 2) only after its group loads of
-  // frame j - 4, issued before R(j - 2)'s slot stores, have returned (vmcnt is in order).
-  // The publish wait counts what every path issues after the slot stores: D(j - 4)'s RD stores
-  // (or row peaks) and the profile store of D(j - 3); tools/check_vmcnt.py proves it on the
-  // built code.  Steps 0-3 and the last three are peeled, every flag a compile-time constant.
+  //   B1 (frame j's reference chirp into LDS) -> staging of group j - 2 (loaded into registers
+  //   during step j - 1) -> B2 -> rows, profile, keys -> publish R(j - 1) (its slot stores waited
+  //   for) -> B3 -> candidates -> R1 | D3 -> the next frame's chirp loads (R1 freed the registers)
+  //   -> wave 0 polls ready(j - 1), every wave loads group k of frame j - 1 -> TD -> T1 | D DFT16
+  //   -> R2 -> T2 -> R3 + slot stores -> RD stores.
+  // The group of frame j - 1 is read about one step after its slot was written, while the
+  // slot's lines are still in the XCD's L2 (a ring of kNS slots: 4 MiB at kNS = 2).
+  // Slot reuse needs no done counters: R(j) writes its slot after this member saw ready(j - 1),
+  // i.e. after every member published R(j - 1); a member publishes R(j - 1) only after its slot
+  // stores of R(j - 1) returned, and its group loads of frame j - 2 were issued before them
+  // (vmcnt retires in order), so every read of frames <= j - 2 is done: kNS >= 2 suffices.
+  // The publish wait counts what every path issues after the slot stores: D(j - 3)'s RD stores
+  // (or row peaks) and the profile store of D(j - 2); tools/check_vmcnt.py proves it on the
+  // built code.  Steps 0-2 and the last two are peeled, every flag a compile-time constant.
   constexpr int kRDs = RD ? 16 : 1;                             // D's stores after the slot stores (RD rows / row peak)
   // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
   auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT) __attribute__((always_inline)) {
     const bool dj = DJ, rj = RJ, pub = PUB, gj = GJ, next = NEXT;
-    const int64_t fd = frame(j - 3);
+    const int64_t fd = frame(j - 2);
     if (j >= 1) __syncthreads();       // B1: step j - 1 done in every wave (transpose regions, keys, x0)
     stamp(0);
 #ifndef XK_NOREF
     if (rj)
       if (j >= 1) put_ref();           // frame j's reference chirp (read by R1 after B3)
 #endif
-    if (gj)   // wave 0 polls (scalar: its vector memory operations stay in flight); B2 releases the rest
-      if (w == 0) wait_ge(&ready[((j - 2) % NS) * 32], (unsigned)(NK * ((j - 2) / NS + 1)), a.xctr + XCD_ABORT, a.xerr);
     if (dj) stage(grp);
     stamp(1);
-    __syncthreads();                   // B2: staged; x0 of frame j in; ready(j - 2) seen
+    __syncthreads();                   // B2: staged; x0 of frame j in
     stamp(2);
     c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
     if (dj) d_rows(fd, xv, x0r, dmu);
@@ -603,10 +610,9 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     // vmcnt waits behind them never wait for an atomic
     if (pub)
       if (lane == 0)
-        __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % NS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
+        __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % kNS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
                                w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     stamp(4);
-    if (gj) ld_group(slot(j - 2) + (int64_t)k * C * GP * kES, grp);
     if (dj) d_cand(fd, xv, x0r);
     stamp(5);
     c2 z0[8], z1[8], u[16];
@@ -620,6 +626,17 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     }
     if (dj) d_a(xv, dmu);
     stamp(6);
+    if (gj) {   // wave 0 polls ready(j - 1) (scalar: its vector memory operations stay in flight) and
+                // tells the other waves through LDS; then every wave loads its share of group k
+      if (w == 0) {
+        wait_ge(&ready[((j - 1) % kNS) * 32], (unsigned)(NK * ((j - 1) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);
+        if (lane == 0) *reinterpret_cast<volatile unsigned*>(&gflag) = (unsigned)j;
+      } else {
+        while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
+      }
+      ld_group(slot(j - 1) + (int64_t)k * C * GP * kES, grp);
+    }
+    stamp(7);
     if (dj) d_td(xv);
     if (rj) {
 #pragma unroll
@@ -633,7 +650,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       for (int a1 = 0; a1 < 16; ++a1) u[a1] = rt[k1 * 136 + a0 + 8 * a1];
       cfence();
     }
-    stamp(7);
     if (rj) {
       c2 q0[8], q1[8];
       r_mid(u);
@@ -648,21 +664,19 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   using F_ = std::false_type;
   using C0 = std::integral_constant<int, 0>;
   using CF = std::integral_constant<int, kRDs + 1>;
-  if (nj >= 4) {
-    //   j       DJ   RJ   PUB  CNT                GJ   NEXT
+  if (nj >= 3) {
+    //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
     body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{});
-    body(1,      F_{}, T_{}, T_{}, C0{},                          F_{}, T_{});
-    body(2,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{});
-    body(3,      T_{}, T_{}, T_{}, std::integral_constant<int, 1>{}, T_{}, T_{});
-    for (int j = 4; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{});
+    body(1,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{});
+    body(2,      T_{}, T_{}, T_{}, std::integral_constant<int, 1>{}, T_{}, T_{});
+    for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{});
     body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{});
-    body(nj + 1, T_{}, F_{}, F_{}, C0{},                          T_{}, F_{});
-    body(nj + 2, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{});
+    body(nj + 1, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{});
   } else {
-    // 1-3 frames on this XCD (launches of < 32 frames): one copy with run-time flags, every
+    // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
     // publish waiting for everything
-    for (int j = 0; j < nj + 3; ++j)
-      body(j, j >= 3, j < nj, j >= 1 && j - 1 < nj, C0{}, j >= 2 && j - 2 < nj, j + 1 < nj);
+    for (int j = 0; j < nj + 2; ++j)
+      body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj, C0{}, j >= 1 && j - 1 < nj, j + 1 < nj);
   }
 #ifdef XK_STAMPS
   if (lane == 0 && (w == 0 || w == 4)) {
