@@ -75,7 +75,7 @@ constexpr bool kSlot16 = true;         // A/B only: fp16 hand-off slots under fp
 constexpr bool kSlot16 = false;
 #endif
 #ifndef XK_RD_AUX
-#define XK_RD_AUX 16                   // RD store cache policy: sc1 (A/B: 17 = sc0 sc1, 2 = nt)
+#define XK_RD_AUX 2                    // RD store cache policy: nt (A/B: 16 = sc1, 17 = sc0 sc1, 18 = sc1 nt, 3 = sc0 nt)
 #endif
 constexpr int kRdAux = XK_RD_AUX;
 #ifndef XK_NS
@@ -533,9 +533,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // or, without an RD map, the row peak (:233)
   auto d_store = [&](int64_t f, const c2 (&xv)[16]) __attribute__((always_inline)) {
     if constexpr (RD) {
-      // RD rows: buffer stores with the sc1 cache policy (the written lines stream out of the
-      // XCD's L2 instead of evicting the hand-off slots; measured 4.93 -> 4.67 ms per 4096
-      // frames against nontemporal global stores)
+      // RD rows: buffer stores with the nt cache policy (with the 2-slot ring: 4.41 vs 4.49 ms per
+      // 4096 frames for sc1, which was the faster one with round 2's 4-slot ring)
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
           static_cast<char*>(a.rd) + f * NR * (int64_t)C * (H ? 4 : 8), (short)0, NR * C * (H ? 4 : 8), 0x00020000);
 #pragma unroll
