@@ -657,6 +657,27 @@ static int build_xcd_tab(fmcw_ctx* c, hipStream_t s) {
   return FMCW_OK;
 }
 
+// fp16 storage on the single pass: the 128-bin blocks of the range cube that hold no bin able
+// to become a detection or slow-time candidate (k_rdx's key test: 1 <= r <= NR - 2 and
+// min_d <= r * dist_per_bin <= max_d, with two bins of margin each side for the local-maximum
+// test's neighbours) are handed between the CUs as c32h; the others stay c64, so the slow-time
+// rows and the profile around a target come from fp32 values.  FMCW_S16=0 keeps every block c64.
+static unsigned host_s16mask(const fmcw_params* p, int NR) {
+  {
+    const char* e = std::getenv("FMCW_S16");
+    if (e && e[0] == '0') return 0u;
+  }
+  const double dpb = p->dist_per_bin;
+  if (!(dpb > 0.0) || !std::isfinite(dpb) || !std::isfinite(p->min_d) || !std::isfinite(p->max_d)) return 0u;
+  const double lo_d = std::floor((double)p->min_d / dpb) - 2, hi_d = std::ceil((double)p->max_d / dpb) + 2;
+  const int lo = (int)std::max(0.0, std::min((double)NR, lo_d));
+  const int hi = (int)std::max(-1.0, std::min((double)NR - 1, hi_d));
+  unsigned m = 0;
+  for (int b = 0; b < NR / 128; ++b)
+    if (hi < lo || 128 * b + 127 < lo || 128 * b > hi) m |= 1u << b;
+  return m;
+}
+
 // Single-pass schedule (kernels_xcd.hip): k_rdx computes range FFT, profile,
 // Doppler FFT and the slow-time candidate rows of each frame, the range cube
 // handed between the CUs of one XCD; k_detect_1p runs the detection; k_slow_fix
@@ -713,6 +734,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
     a.xcube = c->x_cube.as<float2>(); a.xctr = c->x_ctr.as<unsigned>(); a.xerr = c->x_err.as<unsigned>();
     a.slots = slots; a.xtab = c->x_tab.as<float2>(); a.cal_sum = c->cal_sum;
+    a.s16mask = h ? host_s16mask(p, NR) : 0u;
     a.nteams = c->xcd_teams > 0 ? c->xcd_teams : 0;
     std::memcpy(a.xcc_team, c->xcc_team, sizeof(a.xcc_team));
     {

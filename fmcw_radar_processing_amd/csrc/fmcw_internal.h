@@ -91,7 +91,10 @@ struct OnePassArgs {
   unsigned* xerr;          // sticky, reported by fmcw_synchronize: bit 0 a hand-off wait timed out, bit 1 an XCD
                            // got more than 32 blocks (the launch's own abort word lets its grid drain; a later
                            // launch starts with a clear one)
-  int slots;               // hand-off slots per XCD (XCD_MAX_SLOTS)
+  int slots;               // hand-off slots allocated per XCD (XCD_MAX_SLOTS; k_rdx uses 2 of them)
+  unsigned s16mask;        // fp16 storage only: bit b set = range bins 128 b .. 128 b + 127 (groups 4 b .. 4 b + 3)
+                           // are handed over as c32h (X / NR): no bin of the block can become a detection or
+                           // slow-time candidate (host_s16mask in fmcw_api.cpp); 0 = every group c64
   int nteams;              // XCDs of the device (teams of 32 CUs): 8 in SPX mode, 1-4 in the partition modes
   int8_t xcc_team[16];     // HW_REG_XCC_ID -> team index 0..nteams-1, -1 for an XCC not in the device
   const float2* xtab;      // XT_* sections (host, float64, lane order)

@@ -69,11 +69,6 @@ using namespace op;
 #else
 #define XK_REF 1
 #endif
-#ifdef XK_SLOT16
-constexpr bool kSlot16 = true;         // A/B only: fp16 hand-off slots under fp16 storage (fails the STFT bar, below)
-#else
-constexpr bool kSlot16 = false;
-#endif
 #ifndef XK_RD_AUX
 #define XK_RD_AUX 2                    // RD store cache policy: nt (A/B: 16 = sc1, 17 = sc0 sc1, 18 = sc1 nt, 3 = sc0 nt)
 #endif
@@ -217,13 +212,16 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 
   using TP = std::conditional_t<H, h4v, f4v>;
   const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
-  // hand-off slot element: c64 in both storage modes.  (c32h slots holding X / Nr under fp16
-  // storage, XK_SLOT16, run 3.67 vs 4.1 ms per 4096 frames, but the slow-time rows are then
-  // |X| of fp16-rounded values: 4.5e-4 relative, 0.15 dB in the spectrogram against the
-  // 0.05 dB bar of SURVEY 8d, measured at 4096 frames by bench.py's full-size check.)
-  constexpr bool S16 = H && kSlot16;
-  constexpr int kES = S16 ? 4 : 8, kGL = S16 ? 4 : 8;     // bytes per slot element, group loads per thread
+  // hand-off slot element: c64; under fp16 storage the groups of the 128-bin blocks in
+  // a.s16mask hold X / Nr as c32h (half the bytes).  Those blocks hold no bin that can become a
+  // detection or slow-time candidate, so the slow-time rows (and the profile around a target)
+  // still come from fp32 values: all-c32h slots put the slow rows at 4.5e-4 relative and the
+  // 4096-frame spectrogram at 0.15 dB against the 0.05 dB bar of SURVEY 8d.  Every group keeps
+  // the c64 stride in the slot (64 KiB; a c32h group uses its first half).
+  constexpr int kES = 8;
   constexpr int64_t kSlotBytes = (int64_t)NK * C * GP * kES;
+  const unsigned s16m = H ? a.s16mask : 0u;
+  const bool g16 = (s16m >> (k >> 2)) & 1;            // this member's group k is c32h (fixed per member)
   constexpr float kXS = 1.0f / NR, kXU = (float)NR;
 #ifndef XK_NOREF
   // the reference chirp (chirp 0) of the next frame: one sample pair per thread, loaded one
@@ -388,25 +386,22 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     // tools/check_vmcnt.py finds them by that to prove, on the built code, that every publish
     // waits for them
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slot, (short)0, kSlotBytes, 0x00020000);
-    if constexpr (S16) {   // XK_SLOT16: the slot holds X / Nr as c32h (half the bytes of the hand-off)
-      const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 4;
+    // 16-byte stores (cdna_hip_programming.md T21: a store tail is issue-bound per instruction;
+    // 4.69 -> 4.63 ms per 4096 frames against 16 8-byte stores): lane pairs swap one value, the
+    // even lane stores both columns of the e = 0 row, the odd lane both of the e = 1 row
+    const bool odd = lane & 1;
+    const int gl = (lane >> 5) + (odd ? 2 : 0), el = c * GP + (lane & 31) - (odd ? 1 : 0);   // group 4 s2 + gl, element el
 #pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) {
-        const __half2 h0 = __floats2half2_rn(q0[s2].x * kXS, q0[s2].y * kXS);
-        const __half2 h1 = __floats2half2_rn(q1[s2].x * kXS, q1[s2].y * kXS);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h0), rs, o + 4 * s2 * C * GP * 4, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, h1), rs, o + (4 * s2 + 2) * C * GP * 4, 0, 0);
+    for (int s2 = 0; s2 < 8; ++s2) {
+      const f4v v = pair_cols(q0[s2], q1[s2], odd);
+      const int gb = (4 * s2 + gl) * C * GP * 8;
+      if (H && ((s16m >> s2) & 1)) {   // c32h block (wave-uniform): X / Nr, 8 bytes per lane
+        const __half2 h0 = __floats2half2_rn(v.x * kXS, v.y * kXS), h1 = __floats2half2_rn(v.z * kXS, v.w * kXS);
+        __builtin_amdgcn_raw_buffer_store_b64(u2v{__builtin_bit_cast(unsigned, h0), __builtin_bit_cast(unsigned, h1)}, rs,
+                                              gb + el * 4, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, gb + el * 8, 0, 0);
       }
-    } else {
-      const int o = (((lane >> 5) * C + c) * GP + (lane & 31)) * 8;
-      // 16-byte stores (cdna_hip_programming.md T21: a store tail is issue-bound per instruction;
-      // 4.69 -> 4.63 ms per 4096 frames against 16 8-byte stores): lane pairs swap one value, the
-      // even lane stores both columns of the e = 0 row, the odd lane both of the e = 1 row
-      const bool odd = lane & 1;
-      const int ow = odd ? o - 8 + 2 * C * GP * 8 : o;
-#pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2)
-        __builtin_amdgcn_raw_buffer_store_b128(pair_cols(q0[s2], q1[s2], odd), rs, ow + 4 * s2 * C * GP * 8, 0, 0);
     }
   };
 
@@ -415,15 +410,18 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // previous frame); compiler-visible, so its vmcnt bookkeeping covers the data
   // (XK_SLOT16: the group is 32 KiB of c32h, 4 loads per thread, widened and scaled back by Nr
   // into the same fp32 staging image)
-  auto ld_group = [&](const char* __restrict__ grp, f4v (&t)[8]) __attribute__((always_inline)) {
+  // G16 (compile time: the step loop is instantiated per member format): a c32h group is 32 KiB,
+  // 4 loads per thread, widened and scaled back by Nr into the same fp32 staging image
+  auto ld_group = [&](const char* __restrict__ grp, f4v (&t)[8], auto G16) __attribute__((always_inline)) {
+    constexpr int NL = decltype(G16)::value ? 4 : 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(grp), (short)0, C * GP * kES, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < kGL; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
+    for (int i = 0; i < NL; ++i) t[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + 512 * i) * 16, 0, 16);
   };
-  auto stage = [&](const f4v (&t)[8]) __attribute__((always_inline)) {
-    if constexpr (S16) {
+  auto stage = [&](const f4v (&t)[8], auto G16) __attribute__((always_inline)) {
+    if constexpr (decltype(G16)::value) {
 #pragma unroll
-      for (int i = 0; i < kGL; ++i) {
+      for (int i = 0; i < 4; ++i) {
         const int e = tid + 512 * i;            // 16-byte piece: chirp e >> 3, positions 4 (e & 7) .. + 3
         const u4v u = __builtin_bit_cast(u4v, t[i]);
         const float2 a0 = h2f(u.x), a1 = h2f(u.y), a2 = h2f(u.z), a3 = h2f(u.w);
@@ -586,7 +584,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // built code.  Steps 0-2 and the last two are peeled, every flag a compile-time constant.
   constexpr int kRDs = RD ? 16 : 1;                             // D's stores after the slot stores (RD rows / row peak)
   // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
-  auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT) __attribute__((always_inline)) {
+  auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT, auto G16) __attribute__((always_inline)) {
     const bool dj = DJ, rj = RJ, pub = PUB, gj = GJ, next = NEXT;
     const int64_t fd = frame(j - 2);
     if (j >= 1) __syncthreads();       // B1: step j - 1 done in every wave (transpose regions, keys, x0)
@@ -595,7 +593,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     if (rj)
       if (j >= 1) put_ref();           // frame j's reference chirp (read by R1 after B3)
 #endif
-    if (dj) stage(grp);
+    if (dj) stage(grp, G16);
     stamp(1);
     __syncthreads();                   // B2: staged; x0 of frame j in
     stamp(2);
@@ -633,7 +631,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       } else {
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }
-      ld_group(slot(j - 1) + (int64_t)k * C * GP * kES, grp);
+      ld_group(slot(j - 1) + (int64_t)k * C * GP * kES, grp, G16);
     }
     stamp(7);
     if (dj) d_td(xv);
@@ -663,19 +661,27 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   using F_ = std::false_type;
   using C0 = std::integral_constant<int, 0>;
   using CF = std::integral_constant<int, kRDs + 1>;
-  if (nj >= 3) {
-    //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
-    body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{});
-    body(1,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{});
-    body(2,      T_{}, T_{}, T_{}, std::integral_constant<int, 1>{}, T_{}, T_{});
-    for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{});
-    body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{});
-    body(nj + 1, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{});
+  auto run = [&](auto G16) __attribute__((always_inline)) {
+    if (nj >= 3) {
+      //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
+      body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{}, G16);
+      body(1,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{}, G16);
+      body(2,      T_{}, T_{}, T_{}, std::integral_constant<int, 1>{}, T_{}, T_{}, G16);
+      for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{}, G16);
+      body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{}, G16);
+      body(nj + 1, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{}, G16);
+    } else {
+      // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
+      // publish waiting for everything
+      for (int j = 0; j < nj + 2; ++j)
+        body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj, C0{}, j >= 1 && j - 1 < nj, j + 1 < nj, G16);
+    }
+  };
+  if constexpr (H) {
+    if (g16) run(T_{});
+    else run(F_{});
   } else {
-    // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
-    // publish waiting for everything
-    for (int j = 0; j < nj + 2; ++j)
-      body(j, j >= 2, j < nj, j >= 1 && j - 1 < nj, C0{}, j >= 1 && j - 1 < nj, j + 1 < nj);
+    run(F_{});
   }
 #ifdef XK_STAMPS
   if (lane == 0 && (w == 0 || w == 4)) {
