@@ -204,13 +204,11 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
     for (int kk = 0; kk < kn; ++kk) {             // unrolled: the scalar table loads of 4 bins issue together
       const int k = MODE == 3 ? B[k0 + kk] : k0 + kk;
       const auto* Wk = T + (int64_t)k * STFT_W;
-      float re = 0.f, im = 0.f;
+      // (re, im) as one packed accumulator: one v_pk_fma_f32 per tap (the same two fmas)
+      f2t acc = {0.f, 0.f};
 #pragma unroll
-      for (int m = 0; m < STFT_W; ++m) {
-        const f2t wk = Wk[m];
-        re = fmaf(x[m], wk.x, re);
-        im = fmaf(x[m], wk.y, im);
-      }
+      for (int m = 0; m < STFT_W; ++m) acc = __builtin_elementwise_fma(f2t{x[m], x[m]}, Wk[m], acc);
+      const float re = acc.x, im = acc.y;
       const float g = (k == 0 || 2 * k == a.nfft) ? 1.f : 2.f;     // one-sided 'psd'
       const float p = fmaf(re, re, im * im) * scale * g;
       if (valid) lmax = fmaxf(lmax, p);

@@ -597,6 +597,17 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     stamp(1);
     __syncthreads();                   // B2: staged; x0 of frame j in
     stamp(2);
+    c2 z0[8], z1[8], u[16];
+#ifdef XK_RPEARLY   // A/B: R1 right after B2, so the next frame's loads go out before the rows
+    if (rj) r_prep(xin, z0, z1);
+    if (next) {
+      const int jn = j + 1 < nj ? j + 1 : nj - 1;
+#ifndef XK_NOREF
+      ld_ref(frame(jn));
+#endif
+      ld_chirp(frame(jn), xin);
+    }
+#endif
     c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
     if (dj) d_rows(fd, xv, x0r, dmu);
     stamp(3);
@@ -612,7 +623,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     stamp(4);
     if (dj) d_cand(fd, xv, x0r);
     stamp(5);
-    c2 z0[8], z1[8], u[16];
+#ifndef XK_RPEARLY
     if (rj) r_prep(xin, z0, z1);
     if (next) {                        // R1 freed the chirp registers: the next frame's loads go out
       const int jn = j + 1 < nj ? j + 1 : nj - 1;
@@ -621,6 +632,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
       ld_chirp(frame(jn), xin);
     }
+#endif
     if (dj) d_a(xv, dmu);
     stamp(6);
     if (gj) {   // wave 0 polls ready(j - 1) (scalar: its vector memory operations stay in flight) and
@@ -660,15 +672,26 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   using T_ = std::true_type;
   using F_ = std::false_type;
   using C0 = std::integral_constant<int, 0>;
+#ifdef XK_RPEARLY
+  constexpr int kLdN = 8 + (XK_REF ? 1 : 0);                    // the next frame's loads, issued before the publish
+  using CF = std::integral_constant<int, kRDs + kLdN + 1>;
+  using C1 = std::integral_constant<int, kLdN>;
+  using C2 = std::integral_constant<int, kLdN + 1>;
+  using CL = std::integral_constant<int, kRDs + 1>;
+#else
   using CF = std::integral_constant<int, kRDs + 1>;
+  using C1 = std::integral_constant<int, 0>;
+  using C2 = std::integral_constant<int, 1>;
+  using CL = CF;
+#endif
   auto run = [&](auto G16) __attribute__((always_inline)) {
     if (nj >= 3) {
       //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
       body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{}, G16);
-      body(1,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{}, G16);
-      body(2,      T_{}, T_{}, T_{}, std::integral_constant<int, 1>{}, T_{}, T_{}, G16);
+      body(1,      F_{}, T_{}, T_{}, C1{},                          T_{}, T_{}, G16);
+      body(2,      T_{}, T_{}, T_{}, C2{},                          T_{}, T_{}, G16);
       for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{}, G16);
-      body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{}, G16);
+      body(nj,     T_{}, F_{}, T_{}, CL{},                          T_{}, F_{}, G16);
       body(nj + 1, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{}, G16);
     } else {
       // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
