@@ -569,8 +569,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // Step j runs R(j) and D(j - 2) side by side in every wave, so that the range FFT's and the
   // Doppler FFT's dependency chains (DPP sums, LDS transposes) cover each other:
   //   B1 (frame j's reference chirp into LDS) -> staging of group j - 2 (loaded into registers
-  //   during step j - 1) -> B2 -> rows, profile, keys -> publish R(j - 1) (its slot stores waited
-  //   for) -> B3 -> candidates -> R1 | D3 -> the next frame's chirp loads (R1 freed the registers)
+  //   during step j - 1) -> B2 (R(j - 1)'s slot stores waited for) -> publish R(j - 1) -> rows,
+  //   profile, keys -> B3 -> candidates -> R1 | D3 -> the next frame's chirp loads (R1 freed the registers)
   //   -> wave 0 polls ready(j - 1), every wave loads group k of frame j - 1 -> TD -> T1 | D DFT16
   //   -> R2 -> T2 -> R3 + slot stores -> RD stores.
   // The group of frame j - 1 is read about one step after its slot was written, while the
@@ -580,8 +580,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // stores of R(j - 1) returned, and its group loads of frame j - 2 were issued before them
   // (vmcnt retires in order), so every read of frames <= j - 2 is done: kNS >= 2 suffices.
   // The publish wait counts what every path issues after the slot stores: D(j - 3)'s RD stores
-  // (or row peaks) and the profile store of D(j - 2); tools/check_vmcnt.py proves it on the
-  // built code.  Steps 0-2 and the last two are peeled, every flag a compile-time constant.
+  // (or row peaks); tools/check_vmcnt.py proves it on the built code.  Steps 0-2 and the last two are peeled, every flag a compile-time constant.
   constexpr int kRDs = RD ? 16 : 1;                             // D's stores after the slot stores (RD rows / row peak)
   // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
   auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT, auto G16) __attribute__((always_inline)) {
@@ -595,35 +594,27 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
     if (dj) stage(grp, G16);
     stamp(1);
-    __syncthreads();                   // B2: staged; x0 of frame j in
-    stamp(2);
-    c2 z0[8], z1[8], u[16];
-#ifdef XK_RPEARLY   // A/B: R1 right after B2, so the next frame's loads go out before the rows
-    if (rj) r_prep(xin, z0, z1);
-    if (next) {
-      const int jn = j + 1 < nj ? j + 1 : nj - 1;
-#ifndef XK_NOREF
-      ld_ref(frame(jn));
-#endif
-      ld_chirp(frame(jn), xin);
-    }
-#endif
-    c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
-    if (dj) d_rows(fd, xv, x0r, dmu);
-    stamp(3);
-    if (pub) vm_wait<decltype(CNT)::value>();   // R(j - 1)'s slot stores are in the L2
-    if (dj || pub) __syncthreads();    // B3: keys in, staging read out; every wave's R(j - 1) stores done
-    // the publish: wave 0 adds 1 to the slot's ready counter; every other wave adds 0 to a word
-    // of its own, so that every wave issues the same vector-memory operations and the compiler's
-    // vmcnt waits behind them never wait for an atomic
+    // the publish of R(j - 1) at B2: its slot stores (issued at the end of step j - 1, before D(j - 3)'s
+    // RD stores) have had the staging to drain; earlier (at B1) the wait exposes their latency, later
+    // (after the rows, at B3) the other members' polls wait on it (4.31-4.36 vs 4.46 / 4.40 ms)
+    if (pub) vm_wait<decltype(CNT)::value>();
+    __syncthreads();                   // B2: staged; x0 of frame j in; every wave's R(j - 1) slot stores done
+    // wave 0 adds 1 to the slot's ready counter; every other wave adds 0 to a word of its own, so that
+    // every wave issues the same vector-memory operations and the compiler's vmcnt waits behind them
+    // never wait for an atomic
     if (pub)
       if (lane == 0)
         __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % kNS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
                                w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stamp(2);
+    c2 z0[8], z1[8], u[16];
+    c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
+    if (dj) d_rows(fd, xv, x0r, dmu);
+    stamp(3);
+    if (dj) __syncthreads();           // B3: keys in, staging read out
     stamp(4);
     if (dj) d_cand(fd, xv, x0r);
     stamp(5);
-#ifndef XK_RPEARLY
     if (rj) r_prep(xin, z0, z1);
     if (next) {                        // R1 freed the chirp registers: the next frame's loads go out
       const int jn = j + 1 < nj ? j + 1 : nj - 1;
@@ -632,7 +623,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
       ld_chirp(frame(jn), xin);
     }
-#endif
     if (dj) d_a(xv, dmu);
     stamp(6);
     if (gj) {   // wave 0 polls ready(j - 1) (scalar: its vector memory operations stay in flight) and
@@ -672,26 +662,17 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   using T_ = std::true_type;
   using F_ = std::false_type;
   using C0 = std::integral_constant<int, 0>;
-#ifdef XK_RPEARLY
-  constexpr int kLdN = 8 + (XK_REF ? 1 : 0);                    // the next frame's loads, issued before the publish
-  using CF = std::integral_constant<int, kRDs + kLdN + 1>;
-  using C1 = std::integral_constant<int, kLdN>;
-  using C2 = std::integral_constant<int, kLdN + 1>;
-  using CL = std::integral_constant<int, kRDs + 1>;
-#else
-  using CF = std::integral_constant<int, kRDs + 1>;
+  // the publish wait counts D(j - 3)'s RD stores (row peaks), issued after R(j - 1)'s slot stores
   using C1 = std::integral_constant<int, 0>;
-  using C2 = std::integral_constant<int, 1>;
-  using CL = CF;
-#endif
+  using CF = std::integral_constant<int, kRDs>;
   auto run = [&](auto G16) __attribute__((always_inline)) {
     if (nj >= 3) {
       //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
       body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{}, G16);
       body(1,      F_{}, T_{}, T_{}, C1{},                          T_{}, T_{}, G16);
-      body(2,      T_{}, T_{}, T_{}, C2{},                          T_{}, T_{}, G16);
+      body(2,      T_{}, T_{}, T_{}, C1{},                          T_{}, T_{}, G16);
       for (int j = 3; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{}, G16);
-      body(nj,     T_{}, F_{}, T_{}, CL{},                          T_{}, F_{}, G16);
+      body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{}, G16);
       body(nj + 1, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{}, G16);
     } else {
       // 1-2 frames on this XCD (launches of < 24 frames): one copy with run-time flags, every
