@@ -503,15 +503,20 @@ def json_timing(sp, python: bool):
     return out, n
 
 
-def bench_host_path(eng):
+def bench_host_path(eng0):
     """The path MATLAB calls (MEX -> fmcw_process + fmcw_stft on HOST buffers,
     radar_processing.m:197-299): inputs in pageable host memory, PCIe included,
-    at the deployed 64x16 module geometry and at the config-3 geometry."""
+    at the deployed 64x16 module geometry and at the config-3 geometry, on the context the
+    MATLAB drop-in creates (matlab/radar_processing.m: FMCW_DEVICES, else every visible device;
+    frames / STFT segments sharded over its devices)."""
     import torch
     from fmcw_radar_processing_amd import FMCW_C64
     from fmcw_radar_processing_amd import params as P
     from fmcw_radar_processing_amd import windows as W
-    res = {}
+    from fmcw_radar_processing_amd.engine import Engine
+    eng = Engine(None)
+    info = eng.device_info()
+    res = {"context_devices": info["devices"], "rccl": info["rccl"]}
     # one call = one recording, as radar_processing_with_azure.m:50 makes it: the deployed
     # module's 115-frame file, and 256 config-3 frames (512 MiB of IQ, PCIe-bound)
     for name, F, reps in (("deployed_64x16_115_frames", 115, 20), ("config3_256x1024_256_frames", 256, 3)):
@@ -550,6 +555,7 @@ def bench_host_path(eng):
                      "stft_ms": round(ts * 1e3, 3), "h2d_GBps": round(iq.nbytes / tp / 1e9, 2),
                      "what": "fmcw_process (pageable host iq -> pinned 2-slot chunks -> HBM, outputs back) + "
                              "fmcw_stft of the slow-time signal, wall clock"}
+    eng.close()
     return res
 
 

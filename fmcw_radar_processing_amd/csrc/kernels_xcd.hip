@@ -656,7 +656,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       r_end(q0, q1, slot(j));
     }
     stamp(8);
-    if (dj) d_store(fd, xv);
+    if (dj) d_store(fd, xv);           // after R(j)'s slot stores (RD stores before them: 4.64 vs 4.36 ms)
     stamp(9);
   };
   using T_ = std::true_type;
