@@ -426,8 +426,12 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
         const u4v u = __builtin_bit_cast(u4v, t[i]);
         const float2 a0 = h2f(u.x), a1 = h2f(u.y), a2 = h2f(u.z), a3 = h2f(u.w);
         f4v* d = &L.u.stg[(e >> 3) * 17 + (e & 7) * 2];
-        d[0] = f4v{a0.x, a0.y, a1.x, a1.y} * kXU;
-        d[1] = f4v{a2.x, a2.y, a3.x, a3.y} * kXU;
+        const f4v lo = f4v{a0.x, a0.y, a1.x, a1.y} * kXU, hi = f4v{a2.x, a2.y, a3.x, a3.y} * kXU;
+        // lanes 4-7 of each 8-lane store group write their upper half first: the group's 8 stores
+        // then hit 8 different 16-byte bank groups (conflict-free ds_write_b128)
+        const bool sw = (e >> 2) & 1;
+        d[sw ? 1 : 0] = sw ? hi : lo;
+        d[sw ? 0 : 1] = sw ? lo : hi;
       }
     } else {
 #pragma unroll
