@@ -601,7 +601,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     // the publish of R(j - 1) at B2: its slot stores (issued at the end of step j - 1, before D(j - 3)'s
     // RD stores) have had the staging to drain; earlier (at B1) the wait exposes their latency, later
     // (after the rows, at B3) the other members' polls wait on it (4.31-4.36 vs 4.46 / 4.40 ms)
-    if (pub) vm_wait<decltype(CNT)::value>();
+    // (the short-launch copy waits on every path: a wait behind its own `if (pub)` leaves the
+    // path-insensitive proof a path that skips it and still reaches the publish)
+    if constexpr (std::is_same_v<decltype(PUB), bool>) vm_wait<0>();
+    else if (pub) vm_wait<decltype(CNT)::value>();
     __syncthreads();                   // B2: staged; x0 of frame j in; every wave's R(j - 1) slot stores done
     // wave 0 adds 1 to the slot's ready counter; every other wave adds 0 to a word of its own, so that
     // every wave issues the same vector-memory operations and the compiler's vmcnt waits behind them

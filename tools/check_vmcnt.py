@@ -29,6 +29,7 @@ import sys
 INF = float("inf")
 RE_LABEL = re.compile(r"^(\.LBB\d+_\d+|[A-Za-z_][\w.$]*):")
 RE_VMCNT = re.compile(r"vmcnt\((\d+)\)")
+RE_BB = re.compile(r"^;\s*(%bb\.\d+):")
 
 
 def functions(text: str, pattern: str):
@@ -50,17 +51,29 @@ def functions(text: str, pattern: str):
 
 
 def blocks(lines):
-    """[(label, [instr])] in layout order; instructions without comments/directives."""
+    """[(label, [instr])] in layout order; instructions without comments/directives.
+
+    A block starts at every ``.LBB`` label, at every fall-through block LLVM marks
+    only with a ``; %bb.N:`` comment, and after every branch or end: a conditional
+    branch is always the last instruction of its block, so cfg() sees both edges.
+    """
     bl = [("entry", [])]
     for s in lines:
         m = RE_LABEL.match(s)
         if m and s.startswith(".LBB"):
             bl.append((m.group(1), []))
             continue
+        m = RE_BB.match(s)
+        if m:
+            bl.append((m.group(1), []))
+            continue
         s = s.split(";")[0].strip()
         if not s or s.startswith("."):
             continue
         bl[-1][1].append(s)
+        op = s.split()[0]
+        if op == "s_branch" or op.startswith("s_cbranch") or op in ("s_endpgm", "s_setpc_b64"):
+            bl.append((f"{bl[-1][0]}+", []))
     return bl
 
 
@@ -136,7 +149,8 @@ def check_function(name, lines, quiet=False):
                 best[p] = rem
                 work.append((p, len(bl[p][1]), rem, (path + (bl[b][0],))[-6:]))
     if not quiet:
-        margins = ",".join("-" if (b, k) not in worst else str(int(-worst[(b, k)])) for b, k in pubs)
+        margins = ",".join("-" if (b, k) not in worst else
+                           "none" if worst[(b, k)] == INF else str(int(-worst[(b, k)])) for b, k in pubs)
         print(f"{name}: {len(pubs)} publish atomics (margins {margins}), {stores} slot stores, "
               f"{'OK' if not bad else str(len(bad)) + ' uncovered path(s)'}")
     for pub, blk, rem, path in bad[:5]:
