@@ -146,9 +146,10 @@ template <int N> struct FftPlan {
   static constexpr int P = N < 16 ? N : 16;   // values per thread
   static constexpr int T = N / P;             // threads per team
   // LDS padding: one complex every 2^PADSH.  Teams of >= 32 threads (N >= 512) pad one in
-  // 32: the first pass's stores (lane t writes 16 t + r, 16-lane ds_write_b64 groups) and
-  // every pass's loads (32 consecutive elements per 32-lane ds_read_b64 group) are then
-  // conflict-free (a 1-in-16 pad maps elements 0 and 31 of a load onto one bank pair).
+  // 32, so every pass's loads (32 consecutive elements per 32-lane ds_read_b64 group, banks
+  // (a/4) mod 64) are conflict-free (a 1-in-16 pad maps elements 0 and 31 of a load onto one
+  // bank pair).  Their stores (ds_write_b64: 16-lane groups, banks (a/4) mod 32) are
+  // conflict-free when the team index of a lane is team_index<T> (below), not the lane.
   // Smaller teams share 32-lane groups and keep the 1-in-16 pad with odd team strides.
   static constexpr int PADSH = T >= 32 ? 5 : 4;
   static constexpr int LDS = (N < 16) ? 0 : N + (N >> PADSH);  // complex elements of LDS per team
@@ -158,6 +159,22 @@ template <int N> struct FftPlan {
 };
 
 template <int N> __device__ __forceinline__ int lds_pad(int i) { return i + (i >> FftPlan<N>::PADSH); }
+
+// Team index of lane l for teams of T >= 32 threads.  With the 1-in-32 pad, the first pass's
+// store r of index t goes to bank pair (t/2 + r) mod 16 and the second pass's to
+// (t + 8 (t/16 mod 2) + r/2) mod 16: consecutive t put t = 2i and 2i + 1 on one pair (2-way on
+// every first-pass store).  Within each 32-lane block, lanes 0-15 take t = 0, 2, .., 14, 17, 19,
+// .., 31 and lanes 16-31 the rest: one t of every pair {2i, 2i + 1} per 16-lane group, and the
+// second pass's pairs distinct as well.  A permutation inside 32-lane blocks keeps every
+// 32-lane load group on the same consecutive elements and the DPP team sums unchanged.
+template <int T> __device__ __forceinline__ int team_index(int l) {
+  if constexpr (T >= 32) {
+    const int i = l & 31;
+    return (l & ~31) | (2 * (i & 15)) | (((i >> 3) ^ (i >> 4)) & 1);
+  } else {
+    return l;
+  }
+}
 
 constexpr int fft_num_r16(int n) { return n >= 16 ? 1 + fft_num_r16(n / 16) : 0; }
 constexpr int fft_pow16(int k) { return k == 0 ? 1 : 16 * fft_pow16(k - 1); }

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
   }
   __syncthreads();
 
-  const int team = threadIdx.x / T, t0 = threadIdx.x % T;
+  const int team = threadIdx.x / T, t0 = team_index<T>(threadIdx.x % T);   // bank-conflict-free LDS stores
   float2* my = lds + team * LDSN;
   float2* myred = red + team * (T > 64 ? T / 64 : 1);
   const TIn* __restrict__ in = static_cast<const TIn*>(a.iq);
