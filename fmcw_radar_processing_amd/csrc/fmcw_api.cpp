@@ -201,23 +201,60 @@ struct fmcw_ctx {
   DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out, s_bins;
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
   // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one: device calls on
-  // different streams (with different windows or nfft) never share a table
+  // different streams (with different windows or nfft) never share a table.  At most kTabs of
+  // them (a caller that passes a fresh stream per call does not grow device memory): the least
+  // recently used one is taken over, and the new stream first waits for the event recorded
+  // behind the old owner's last readers (stft_tab_done), so its rewrite cannot overtake them
+  // -- the event outlives a destroyed stream.
   struct StreamTab {
-    hipStream_t s;
+    hipStream_t s = nullptr;
     DevBuf t;
+    hipEvent_t done = nullptr;
+    uint64_t tick = 0;
+    ~StreamTab() {
+      if (done) (void)hipEventDestroy(done);
+    }
   };
+  static constexpr size_t kTabs = 8;
   std::vector<std::unique_ptr<StreamTab>> s_tabs;
+  uint64_t tab_tick = 0;
   float2* stft_tab(hipStream_t st, size_t bytes, int* status) {
     StreamTab* e = nullptr;
     for (auto& x : s_tabs)
       if (x->s == st) e = x.get();
-    if (!e) {
+    if (!e && s_tabs.size() < kTabs) {
       s_tabs.push_back(std::make_unique<StreamTab>());
       e = s_tabs.back().get();
       e->s = st;
+    } else if (!e) {
+      e = s_tabs[0].get();
+      for (auto& x : s_tabs)
+        if (x->tick < e->tick) e = x.get();
+      if (e->done && hipStreamWaitEvent(st, e->done, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        *status = fail(FMCW_E_HIP, "STFT table: hipStreamWaitEvent failed");
+        return nullptr;
+      }
+      e->s = st;
     }
+    e->tick = ++tab_tick;
     *status = e->t.ensure(bytes);
     return e->t.as<float2>();
+  }
+  // after the kernels that read stream st's table are enqueued
+  int stft_tab_done(hipStream_t st) {
+    for (auto& x : s_tabs) {
+      if (x->s != st) continue;
+      if (!x->done && hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FMCW_E_HIP, "STFT table: hipEventCreate failed");
+      }
+      if (hipEventRecord(x->done, st) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(FMCW_E_HIP, "STFT table: hipEventRecord failed");
+      }
+    }
+    return FMCW_OK;
   }
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
@@ -1028,6 +1065,7 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
     CHK(st);
     HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
     HIPCHK(fmcw::launch_stft20(a, tab, d_P ? 0 : 1, nullptr, s));
+    CHK(c->stft_tab_done(s));
   } else {
     HIPCHK(fmcw::launch_stft_power(a, s));
   }
@@ -1062,6 +1100,7 @@ int fmcw_stft_db_direct_device(fmcw_ctx* c, const float* d_slow, const int32_t* 
   CHK(st);
   HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
   HIPCHK(fmcw::launch_stft20(a, tab, 2, d_out, s));
+  CHK(c->stft_tab_done(s));
   tm.done();
   return FMCW_OK;
 }
@@ -1281,6 +1320,7 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table on s
       CHK(st);
       HIPCHK(fmcw::launch_stft20(a, tab, 3, d->s_P.as<float>(), s));
+      CHK(d->stft_tab_done(s));
       tm.done();
     }
     HIPCHK(hipStreamSynchronize(s));   // the host-side scalars above go out of scope

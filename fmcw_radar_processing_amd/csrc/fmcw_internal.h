@@ -253,11 +253,6 @@ struct RenderArgs {
 };
 hipError_t launch_render(const RenderArgs& a, hipStream_t s);
 
-// png_writer.cpp: indexed PNG of [H][1 + W] rows (filter byte first), jet(256) palette
-int png_write_indexed(const char* path, const uint8_t* rows, int W, int H, int level, int threads, int64_t* bytes);
-void jet_palette(uint8_t* rgb);
-
-// thread-local error text of fmcw_last_error (fmcw_api.cpp); returns code
-int set_error(int code, const char* msg);
-
 }  // namespace fmcw
+
+#include "host_io.h"   // png_write_indexed, jet_palette, set_error

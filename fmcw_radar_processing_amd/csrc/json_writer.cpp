@@ -14,7 +14,7 @@
 //   MxN -> array of M row arrays; empty -> []
 //   NaN / Inf -> null; integral |v| < 1e15 -> integer text; else %.15g
 #include "../../include/fmcw.h"
-#include "fmcw_internal.h"
+#include "host_io.h"
 
 #include <algorithm>
 #include <charconv>

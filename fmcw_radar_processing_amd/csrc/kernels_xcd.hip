@@ -747,25 +747,32 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   if (a.nteams < 1 || a.nteams > 8) return hipErrorInvalidValue;
   const dim3 g(xk::NK * a.nteams), bl(64 * xk::NW);
+  // Cooperative launch: the runtime checks the grid against the occupancy query and refuses
+  // (hipErrorCooperativeLaunchTooLarge) a grid it cannot make resident at once, instead of
+  // dispatching blocks that would wait for a CU that never frees.  Residency against kernels
+  // of other streams or processes is not part of that check: the bounded waits cover it
+  // (tests/test_gpu_coresidency.py).  FMCW_XCD_PLAIN_LAUNCH=1 takes a plain launch (A/B).
+  static const bool plain = [] { const char* v = std::getenv("FMCW_XCD_PLAIN_LAUNCH"); return v && v[0] == '1'; }();
+  auto go = [&](auto kern) {
+    if (plain) {
+      hipLaunchKernelGGL(kern, g, bl, 0, s, a);
+      return hipGetLastError();
+    }
+    void* args[] = {const_cast<OnePassArgs*>(&a)};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kern), g, bl, args, 0, s);
+  };
   const bool rd = a.rd != nullptr;
   if (a.S == op::NR) {
-    if (a.h) {
-      if (rd) hipLaunchKernelGGL((k_rdx<true, true, true>), g, bl, 0, s, a);
-      else hipLaunchKernelGGL((k_rdx<true, true, false>), g, bl, 0, s, a);
-    } else {
-      if (rd) hipLaunchKernelGGL((k_rdx<true, false, true>), g, bl, 0, s, a);
-      else hipLaunchKernelGGL((k_rdx<true, false, false>), g, bl, 0, s, a);
-    }
+    if (a.h) e = rd ? go(k_rdx<true, true, true>) : go(k_rdx<true, true, false>);
+    else e = rd ? go(k_rdx<true, false, true>) : go(k_rdx<true, false, false>);
   } else {
-    if (a.h) {
-      if (rd) hipLaunchKernelGGL((k_rdx<false, true, true>), g, bl, 0, s, a);
-      else hipLaunchKernelGGL((k_rdx<false, true, false>), g, bl, 0, s, a);
-    } else {
-      if (rd) hipLaunchKernelGGL((k_rdx<false, false, true>), g, bl, 0, s, a);
-      else hipLaunchKernelGGL((k_rdx<false, false, false>), g, bl, 0, s, a);
-    }
+    if (a.h) e = rd ? go(k_rdx<false, true, true>) : go(k_rdx<false, true, false>);
+    else e = rd ? go(k_rdx<false, false, true>) : go(k_rdx<false, false, false>);
   }
-  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return e;
+  }
   return hipEventRecord(xcd_chain_ev[dev], s);
 }
 

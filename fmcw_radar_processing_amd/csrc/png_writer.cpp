@@ -7,11 +7,12 @@
 // ended by a sync flush, concatenated, with the adler32 of the whole image
 // combined from the strips' -- which is one valid zlib stream (the pigz method).
 #include "../../include/fmcw.h"
-#include "fmcw_internal.h"
+#include "host_io.h"
 
 #include <zlib.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <string>
 #include <thread>

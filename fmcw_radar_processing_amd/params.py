@@ -134,6 +134,27 @@ def derive_params(device: dict, nr: int = 256, nd: int = 16, mode: str = PARITY,
     return cfg
 
 
+def fp16_fp32_bins(cfg: FmcwConfig) -> np.ndarray:
+    """Range bins whose hand-off stays fp32 under fp16 storage on the XCD-team schedule: the
+    128-bin blocks that hold a bin able to become a detection or slow-time candidate (min_d /
+    max_d of :126-127, two bins of margin); the other blocks travel as c32h X / Nr.  Mirror of
+    fmcw_api.cpp host_s16mask (float32 parameters as the C-ABI carries them), for checks that
+    hold the profile in those blocks, and the target magnitudes, to the fp32 bar."""
+    nr = cfg.nr
+    dpb = float(np.float32(cfg.dist_per_bin))
+    keep = np.ones(nr, bool)
+    if not (dpb > 0 and np.isfinite(dpb)) or nr % 128:
+        return keep
+    lo_d = np.floor(float(np.float32(cfg.min_d)) / dpb) - 2
+    hi_d = np.ceil(float(np.float32(cfg.max_d)) / dpb) + 2
+    lo = int(max(0.0, min(float(nr), lo_d)))
+    hi = int(max(-1.0, min(float(nr - 1), hi_d)))
+    for b in range(nr // 128):
+        if hi < lo or 128 * b + 127 < lo or 128 * b > hi:
+            keep[128 * b: 128 * b + 128] = False
+    return keep
+
+
 def calibration(calib_data: np.ndarray, n_rx: int, nts: int) -> np.ndarray:
     """:166-174 calib_rx1 = (I(1:dec:N_cal) + 1i*Q(1:dec:N_cal)).'"""
     calib_data = np.asarray(calib_data, dtype=np.float64).reshape(-1)

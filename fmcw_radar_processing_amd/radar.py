@@ -134,6 +134,30 @@ def write_outputs_no(out_dir: str, filename: str, cfg: P.FmcwConfig, per: dict, 
 # ---------------------------------------------------------------------------
 # the entry point (GPU)
 # ---------------------------------------------------------------------------
+_DEFAULT_ENGINE = None
+
+
+def _default_engine():
+    """The per-process context of calls that pass no engine, created once (as the MEX gateway's
+    static context: mexLock on create, mexAtExit destroy).  Devices: FMCW_DEVICES when it is set
+    (fmcw_default_devices), else GPU 0 only -- a deployed 115-frame file does not pay for a
+    context and an RCCL communicator on every GPU of the node, and takes no GPU it was not given."""
+    global _DEFAULT_ENGINE
+    if _DEFAULT_ENGINE is None:
+        import atexit
+        from .engine import Engine
+        _DEFAULT_ENGINE = Engine(None if os.environ.get("FMCW_DEVICES") else 0)
+        atexit.register(_drop_default_engine)
+    return _DEFAULT_ENGINE
+
+
+def _drop_default_engine():
+    global _DEFAULT_ENGINE
+    eng, _DEFAULT_ENGINE = _DEFAULT_ENGINE, None
+    if eng is not None:
+        eng.close()
+
+
 def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_data: np.ndarray,
                      device: dict, fdata: str = "radar_data", out_dir: str = ".", engine=None,
                      upload: Callable[[str], None] | None = None, nr: int = 256, nd: int = 16,
@@ -146,29 +170,22 @@ def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_
     Returns the paths written and the intermediate arrays.  Raises where
     MATLAB raises (e.g. spectrogram of fewer than 20 slow-time samples).
     """
-    from .engine import Engine
-
     filename = os.path.splitext(os.path.basename(fdata))[0]            # :68
     cfg = P.derive_params(device, nr=nr, nd=nd, mode=mode)             # :89-154
     cal = P.calibration(calib_data, cfg.n_rx, cfg.nts)                 # :166-174
     frames = np.asarray(frames)
     F = frames.shape[0]
-    own = engine is None
-    eng = Engine(None) if own else engine                              # FMCW_DEVICES or every GPU
-    try:
-        eng.set_taps(cfg, cal)                                         # :138-139 windows
-        flag = str(process_animal_activity).lower()
-        if flag == "no":
-            res = _run_no(eng, cfg, frames, F, filename, out_dir, upload)
-        elif flag == "yes":
-            res = _run_yes(eng, cfg, frames, F, filename, out_dir, upload)
-        else:
-            res = {"paths": []}                                         # :195/:440: neither branch
-        res["devices"] = list(eng.devices)                              # the GPUs this call drove
-        return res
-    finally:
-        if own:
-            eng.close()
+    eng = _default_engine() if engine is None else engine              # FMCW_DEVICES, else GPU 0
+    eng.set_taps(cfg, cal)                                             # :138-139 windows
+    flag = str(process_animal_activity).lower()
+    if flag == "no":
+        res = _run_no(eng, cfg, frames, F, filename, out_dir, upload)
+    elif flag == "yes":
+        res = _run_yes(eng, cfg, frames, F, filename, out_dir, upload)
+    else:
+        res = {"paths": []}                                            # :195/:440: neither branch
+    res["devices"] = list(eng.devices)                                 # the GPUs this call drove
+    return res
 
 
 def _run_no(eng, cfg, frames, F, filename, out_dir, upload):

@@ -38,7 +38,9 @@
 extern "C" {
 #endif
 
-#define FMCW_ABI_VERSION 2
+/* 3: FMCW_PIPE_ONEPASS names the XCD-team schedule (E_ARG where the XCD census fails),
+ *    fmcw_default_devices, FMCW_JSON_BOOL, k_rdx launched cooperatively */
+#define FMCW_ABI_VERSION 3
 
 typedef enum fmcw_status {
   FMCW_OK = 0,

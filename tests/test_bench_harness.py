@@ -41,6 +41,26 @@ def test_gpus_2_launches_two_ranks():
     assert d["n_gpus"] == 2 and d["ranks_reduced"] == 2
 
 
+def test_gpus_2_names_config5_and_the_frame_total():
+    """with N > 1 ranks the line names BASELINE config 5 and the frames the
+    run covered; --stream-frames 65536 makes the run the whole config-5 stream (8 steps on 2)."""
+    r = _run_bench(["--gpus", "2", "--dry-dist", "--stream-frames", "65536"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    c = d["config"]
+    assert c["workload"].startswith("BASELINE config 5") and "65536-frame" in c["workload"]
+    assert d["steps"] == 8 and c["frames_total_per_run"] == 65536 and c["covers_config5_stream"]
+    assert c["parallelism"] == "frame-shard dp2" and c["frames_per_gpu"] == 4096
+    one = bench.config_block(1, 4096, 20)
+    assert one["workload"].startswith("BASELINE config 4") and one["frames_total_per_run"] == 81920
+    assert bench.config_block(8, 4096, 2)["covers_config5_stream"]
+
+
+def test_stream_frames_must_divide():
+    r = _run_bench(["--gpus", "2", "--dry-dist", "--stream-frames", "65537"])
+    assert r.returncode == 2 and "not a multiple" in r.stderr
+
+
 def test_world_size_must_match_gpus():
     r = _run_bench(["--gpus", "2", "--dry-dist"], env_extra={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2

@@ -62,6 +62,7 @@ def test_branch_around_the_wait_fails(marker):
     s_cbranch_scc1 .LBB0_2
 {marker}    s_waitcnt vmcnt(0)
 .LBB0_2:
+    s_barrier
     global_atomic_add v17, v18, s[8:9]
     s_endpgm
 """)
@@ -78,9 +79,60 @@ def test_wait_on_both_branches_passes():
     global_load_dword v5, v[12:13], off nt
     s_waitcnt vmcnt(1)
 .LBB0_3:
+    s_barrier
     global_atomic_add v17, v18, s[8:9]
     s_endpgm
 """)
+
+
+def test_wait_after_the_barrier_fails():
+    # wave 0's add publishes every wave's stores: a wait between the barrier and the add
+    # covers the adding wave only
+    assert not _run("""
+    buffer_store_dwordx4 v[0:3], v4, s[0:3], 0 offen
+    s_barrier
+    s_waitcnt vmcnt(0)
+    global_atomic_add v17, v18, s[8:9]
+    s_endpgm
+""")
+
+
+def test_relaxed_far_branch_fails():
+    # s_getpc/s_add/s_setpc (LLVM branch relaxation): an edge the CFG walk cannot see
+    assert not _run("""
+    buffer_store_dwordx4 v[0:3], v4, s[0:3], 0 offen
+    s_waitcnt vmcnt(0)
+    s_barrier
+    s_getpc_b64 s[10:11]
+    s_add_u32 s10, s10, 0x40
+    s_addc_u32 s11, s11, 0
+    s_setpc_b64 s[10:11]
+    global_atomic_add v17, v18, s[8:9]
+    s_endpgm
+""")
+
+
+@pytest.mark.parametrize("wait", [True, False])
+def test_relaxed_far_branch_is_followed(wait):
+    # LLVM's relaxed form of a far branch: its target edge is followed like an s_branch, so a
+    # relaxed branch around the wait is caught and one through it passes
+    w = "    s_waitcnt vmcnt(0)\n" if wait else ""
+    assert _run(f"""
+    buffer_store_dwordx4 v[0:3], v4, s[0:3], 0 offen
+{w}    s_cbranch_scc0 .LBB0_12
+; %bb.9:
+    s_getpc_b64 s[98:99]
+.Lpost_getpc0:
+    s_add_u32 s98, s98, (.LBB0_20-.Lpost_getpc0)&4294967295
+    s_addc_u32 s99, s99, (.LBB0_20-.Lpost_getpc0)>>32
+    s_setpc_b64 s[98:99]
+.LBB0_12:
+    s_waitcnt vmcnt(0)
+.LBB0_20:
+    s_barrier
+    global_atomic_add v17, v18, s[8:9]
+    s_endpgm
+""") == wait
 
 
 def test_policy_stores_are_not_slot_stores():

@@ -14,8 +14,13 @@ on every control-flow path into every no-return ``global_atomic_add`` (the
 publishes), that each slot store -- a ``buffer_store_*`` without a cache-policy
 flag; k_rdx issues no other such stores -- is covered by some wait on the way: between the store and
 that wait at least N vector-memory operations were issued.  A path with no
-slot store (the first steps) is fine.  Calls are treated as issuing nothing
-and waiting for nothing (conservative).  Exit status 1 on any uncovered path:
+slot store (the first steps) is fine.  Wave 0's add publishes every wave's stores, so a wait
+counts only when it comes BEFORE the last ``s_barrier`` ahead of the publish (every wave
+runs the same code: its wait then precedes the barrier wave 0 crosses before adding); a
+wait between that barrier and the add covers the adding wave alone.  Calls are treated
+as issuing nothing and waiting for nothing (conservative), and an ``s_setpc_b64`` inside
+a k_rdx body (branch relaxation of a far branch: a CFG edge this script cannot follow)
+fails the check.  Exit status 1 on any uncovered path:
 the Makefile then fails the build, so a compiler change that splits, merges or
 reorders a store cannot silently publish a slot before its bytes are in L2.
 
@@ -89,6 +94,22 @@ def is_vmem(ins: str) -> bool:
     return op.startswith(("global_", "buffer_", "scratch_", "flat_")) and op not in ("buffer_inv",)
 
 
+RE_RELAX = re.compile(r"^s_add_u32\s+(s\d+),\s*\1,\s*\((\.LBB\d+_\d+)-\.Lpost_getpc\d+\)")
+
+
+def relaxed_target(ins):
+    """Target label of LLVM's relaxed far branch (s_getpc_b64 s[a:b]; s_add_u32 sa, sa,
+    (.LBBx_y-.Lpost_getpcN)&...; s_addc_u32; s_setpc_b64 s[a:b]) ending the block, else None."""
+    if not ins or not ins[-1].startswith("s_setpc_b64"):
+        return None
+    reg = re.search(r"s\[(\d+):\d+\]", ins[-1])
+    for s in reversed(ins[:-1]):
+        m = RE_RELAX.match(s)
+        if m and reg and m.group(1) == f"s{reg.group(1)}":
+            return m.group(2)
+    return None
+
+
 def cfg(bl):
     idx = {lab: i for i, (lab, _) in enumerate(bl)}
     succ = []
@@ -98,6 +119,8 @@ def cfg(bl):
         nxt = [i + 1] if i + 1 < len(bl) else []
         if op == "s_branch":
             succ.append([idx[last[1]]])
+        elif op == "s_setpc_b64" and relaxed_target(ins) in idx:
+            succ.append([idx[relaxed_target(ins)]])     # a relaxed far branch: s_branch in effect
         elif op.startswith("s_cbranch"):
             succ.append([idx[last[1]]] + nxt)
         elif op in ("s_endpgm", "s_setpc_b64"):
@@ -117,21 +140,30 @@ def check_function(name, lines, quiet=False):
     pubs = [(b, k) for b, (_, ins) in enumerate(bl) for k, s in enumerate(ins)
             if s.startswith("global_atomic_add") and " sc0" not in s and " glc" not in s]
     stores = sum(1 for _, ins in bl for s in ins if is_slot_store(s))
+    unresolved = [lab for lab, ins in bl if ins and ins[-1].startswith("s_setpc_b64") and relaxed_target(ins) is None]
+    if unresolved:
+        if not quiet:
+            print(f"{name}: s_setpc_b64 in block {unresolved[0]} with no s_getpc/s_add_u32 target: "
+                  "the CFG is not followed, FAIL")
+        return False
     bad = []
     worst = {}
     for b0, k0 in pubs:
         # backward search; state = the smallest "still needed" count over the waits passed
-        # (larger = worse); a block is re-walked only with a worse state than before
+        # (larger = worse) and whether the walk has crossed an s_barrier yet (only waits behind
+        # one count); a block is re-walked only with a worse state than before
         best = {}
-        work = [(b0, k0, INF, ())]
+        work = [(b0, k0, INF, False, ())]
         while work:
-            b, k, rem, path = work.pop()
+            b, k, rem, crossed, path = work.pop()
             ins = bl[b][1]
             hit = False
             for i in range(k - 1, -1, -1):
                 s = ins[i]
+                if s.startswith("s_barrier"):
+                    crossed = True
                 m = RE_VMCNT.search(s) if s.startswith("s_waitcnt") else None
-                if m:
+                if m and crossed:
                     rem = min(rem, int(m.group(1)))
                 if is_slot_store(s):
                     if rem > 0:
@@ -144,10 +176,10 @@ def check_function(name, lines, quiet=False):
             if hit:
                 continue
             for p in pred[b]:
-                if p in best and best[p] >= rem:
+                if (p, crossed) in best and best[(p, crossed)] >= rem:
                     continue
-                best[p] = rem
-                work.append((p, len(bl[p][1]), rem, (path + (bl[b][0],))[-6:]))
+                best[(p, crossed)] = rem
+                work.append((p, len(bl[p][1]), rem, crossed, (path + (bl[b][0],))[-6:]))
     if not quiet:
         margins = ",".join("-" if (b, k) not in worst else
                            "none" if worst[(b, k)] == INF else str(int(-worst[(b, k)])) for b, k in pubs)

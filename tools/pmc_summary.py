@@ -155,11 +155,14 @@ def main(d, json_out=None, bench_log=None):
                  "hbm_bytes_per_launch": int((2 * r["FETCH_SIZE"] + r["WRITE_SIZE"]) * 1024)}
             if k in stat_us:
                 e["rocprof_avg_us"], e["rocprof_calls"] = round(stat_us[k][0], 2), stat_us[k][1]
-            kb = (bench.get("kernels") or {}).get(lb)
-            if kb:
-                e["frames_per_launch"] = kb["frames_per_launch"]
-                e["bench_event_avg_us"] = kb["avg_launch_us"]
-            out["kernels"][lb] = e
+            # keyed by the full instantiation name: k_rdx<.., H = true, ..> (fp16 storage) and the fp32
+            # k_rdx share the label, and one must not overwrite the other; the bench's event time is
+            # attached only to the instantiation its roofline names
+            e["label"] = lb
+            if k in roofs:
+                e["frames_per_launch"] = roofs[k]["frames_per_launch"]
+                e["bench_event_avg_us"] = roofs[k]["avg_launch_us"]
+            out["kernels"][k] = e
         with open(json_out, "w") as fh:
             json.dump(out, fh, indent=1)
         print(f"wrote {json_out}")
