@@ -747,14 +747,18 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   if (a.nteams < 1 || a.nteams > 8) return hipErrorInvalidValue;
   const dim3 g(xk::NK * a.nteams), bl(64 * xk::NW);
-  // Cooperative launch: the runtime checks the grid against the occupancy query and refuses
-  // (hipErrorCooperativeLaunchTooLarge) a grid it cannot make resident at once, instead of
-  // dispatching blocks that would wait for a CU that never frees.  Residency against kernels
-  // of other streams or processes is not part of that check: the bounded waits cover it
-  // (tests/test_gpu_coresidency.py).  FMCW_XCD_PLAIN_LAUNCH=1 takes a plain launch (A/B).
-  static const bool plain = [] { const char* v = std::getenv("FMCW_XCD_PLAIN_LAUNCH"); return v && v[0] == '1'; }();
+  // Residency.  The grid (one 512-thread block per CU) is checked against the occupancy query
+  // once per context (xcd_census: every k_rdx instantiation must fit one block per CU, else
+  // AUTO takes the streams schedule); kernels of other streams or processes that hold CUs are
+  // covered by the bounded waits (FMCW_E_HIP, tests/test_gpu_coresidency.py).  A cooperative
+  // launch makes the same check per launch, but on MI355X / ROCm 7.2 it measured 4.69-4.70 ms
+  // per 4096 frames against 4.32 for the plain launch, and the detection, compaction and STFT
+  // kernels behind it on the stream 3-8x slower (profiles/r04c_coop_ab.txt), so it is opt-in:
+  // FMCW_XCD_COOP=1.
+  const char* coop_env = std::getenv("FMCW_XCD_COOP");   // read per launch (tests switch it)
+  const bool coop = coop_env && coop_env[0] == '1';
   auto go = [&](auto kern) {
-    if (plain) {
+    if (!coop) {
       hipLaunchKernelGGL(kern, g, bl, 0, s, a);
       return hipGetLastError();
     }
@@ -788,6 +792,22 @@ hipError_t xcd_census(int* nteams, int8_t* xcc_team) {
   if (cus < xk::NK || cus > XCD_GRID || cus % xk::NK) {
     if (dbg) std::fprintf(stderr, "xcd_census: %d CUs\n", cus);
     return hipSuccess;
+  }
+  // every k_rdx instantiation must be resident at one 512-thread block per CU (what a
+  // cooperative launch would check per launch)
+  {
+    const void* ks[] = {reinterpret_cast<const void*>(k_rdx<true, false, true>), reinterpret_cast<const void*>(k_rdx<true, false, false>),
+                        reinterpret_cast<const void*>(k_rdx<true, true, true>), reinterpret_cast<const void*>(k_rdx<true, true, false>),
+                        reinterpret_cast<const void*>(k_rdx<false, false, true>), reinterpret_cast<const void*>(k_rdx<false, false, false>),
+                        reinterpret_cast<const void*>(k_rdx<false, true, true>), reinterpret_cast<const void*>(k_rdx<false, true, false>)};
+    for (const void* kf : ks) {
+      int nb = 0;
+      if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, 64 * xk::NW, 0)) != hipSuccess) return e;
+      if (nb < 1) {
+        if (dbg) std::fprintf(stderr, "xcd_census: k_rdx not resident at one block per CU\n");
+        return hipSuccess;
+      }
+    }
   }
   int* d = nullptr;
   if ((e = hipMalloc(&d, XCD_GRID * sizeof(int))) != hipSuccess) return e;

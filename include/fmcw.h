@@ -39,7 +39,7 @@ extern "C" {
 #endif
 
 /* 3: FMCW_PIPE_ONEPASS names the XCD-team schedule (E_ARG where the XCD census fails),
- *    fmcw_default_devices, FMCW_JSON_BOOL, k_rdx launched cooperatively */
+ *    fmcw_default_devices, FMCW_JSON_BOOL */
 #define FMCW_ABI_VERSION 3
 
 typedef enum fmcw_status {

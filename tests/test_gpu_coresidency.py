@@ -1,9 +1,10 @@
 """k_rdx beside another resident kernel.
 
 k_rdx's 256 workgroups wait on each other (the XCD-team hand-off of kernels_xcd.hip), so they
-must be resident together.  It is launched cooperatively (the runtime checks the grid against
-the occupancy query), but a kernel of ANOTHER stream that holds a CU is outside that check --
-the RCCL kernels of a torchrun job, or another process.  Here a single-wave spin kernel
+must be resident together.  The context checks the grid against the occupancy query once (a
+cooperative launch would check it per launch, FMCW_XCD_COOP=1, and is run here too), but a
+kernel of ANOTHER stream that holds a CU is outside that check -- the RCCL kernels of a
+torchrun job, or another process.  Here a single-wave spin kernel
 (torch.cuda._sleep) on a second stream holds one CU while k_rdx runs on the first: one k_rdx
 workgroup cannot start until the spin ends (k_rdx's 2 waves x 256 VGPRs fill every SIMD).
 The contract: either the outputs equal those of an undisturbed run bit for bit (the blocked
@@ -43,9 +44,11 @@ def _host(outs, d_rd):
     return {k: v.cpu().numpy() for k, v in outs.items()} | {"rd": d_rd.cpu().numpy()}
 
 
+@pytest.mark.parametrize("coop", [False, True])
 @pytest.mark.parametrize("hold_s", [0.25, 2.5])
-def test_rdx_beside_a_resident_kernel(engine, hold_s):
+def test_rdx_beside_a_resident_kernel(engine, monkeypatch, hold_s, coop):
     import torch
+    monkeypatch.setenv("FMCW_XCD_COOP", "1" if coop else "0")
     cfg, p, wr, wd, cal = case(1024, 256, 1024, 256, P.THROUGHPUT)
     engine.set_taps(cfg, cal, wr, wd)
     engine.set_pipeline(_lib.FMCW_PIPE_XCD)
