@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--stream-frames", type=int, default=0,
                     help="BASELINE config 5: set --steps so that the run covers exactly this many frames over "
                          "all GPUs (65536 = the config-5 stream: 16 steps on 1 GPU, 2 on 8)")
+    ap.add_argument("--stft-form", choices=["direct", "stored"], default="stored",
+                    help="dB of the STFT leg: stored = pass 1 writes P and max(P), pass 2 turns P into dB in "
+                         "place (0.154 ms per step); direct = pass 1 max(P) only, pass 2 recomputes P and "
+                         "writes dB (0.171 ms; profiles/r04d_stft_ab.txt)")
     ap.add_argument("--dry-dist", action="store_true",
                     help="launcher test without a GPU: the ranks meet over gloo and rank 0 prints n_gpus")
     return ap.parse_args()
@@ -202,17 +206,8 @@ def main():
             lens = fdist.all_lengths(d_len)
             head = fdist.head_samples(outs["slow_mag"], flist, d_len, h)
             hbuf, hl = fdist.right_halo(head, lens, rank)
-        pmax.zero_()
-        # two-pass STFT without a stored P: pass 1 forms max(P) only, pass 2 recomputes P and
-        # writes 20 log10(P / max) (:276-283) -- P never goes to HBM and back
-        eng.stft_power_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
-                              max_seg, None, pmax, nseg, d_halo=hbuf, n_halo=h if world > 1 else 0,
-                              d_halo_len=hl, stream=stream)
-        if world > 1:
-            fdist.global_max_(pmax)
-        eng.stft_db_direct_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
-                                  max_seg, pmax, d_P, d_halo=hbuf, n_halo=h if world > 1 else 0, d_halo_len=hl,
-                                  stream=stream)
+        stft_leg(eng, args.stft_form, outs["slow_mag"], flist, d_len, C, win, fs, max_seg, d_P, pmax, nseg,
+                 hbuf, hl, h if world > 1 else 0, fdist.global_max_ if world > 1 else None, stream)
         if world > 1:
             fdist.gather_range_speed(outs["tgt_count"], outs["tgt_range_idx"], outs["tgt_doppler_idx"],
                                      outs["tgt_range_mag"])
@@ -345,7 +340,7 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f16-storage/f32-compute" if args.fp16 else "f32",
             "data": "synthetic (SURVEY.md 8d generator, generated in HBM per rank)",
-            "config": config_block(world, F, args.steps, C, S, NR, ND),
+            "config": dict(config_block(world, F, args.steps, C, S, NR, ND), stft_form=args.stft_form),
             "hbm_alg_GBps": round(alg_per_frame * value / world / 1e9, 1),
             "roofline": roof,
             "path_roofline": path,
@@ -365,6 +360,25 @@ def main():
     if not ok:
         print("bench.py: the full-size check against the oracle FAILED (see \"checked\")", file=sys.stderr, flush=True)
         sys.exit(1)
+
+
+def stft_leg(eng, form, slow, flist, d_len, C, win, fs, max_seg, d_P, pmax, nseg, hbuf, hl, n_halo, gmax, stream):
+    """The STFT leg of a step (:270-283) over the compacted slow-time rows; d_P ends as the dB map.
+    stored: pass 1 writes P (:276) and max(P), pass 2 turns P into 20 log10(P / max) in place;
+    direct: pass 1 forms max(P) only, pass 2 recomputes P and writes the dB.  gmax: the
+    all_reduce(MAX) of max(P) across ranks (dist.py), between the passes."""
+    pmax.zero_()
+    stored = form == "stored"
+    eng.stft_power_device(slow, flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs, max_seg,
+                          d_P if stored else None, pmax, nseg, d_halo=hbuf, n_halo=n_halo, d_halo_len=hl,
+                          stream=stream)
+    if gmax is not None:
+        gmax(pmax)
+    if stored:
+        eng.stft_db_device(d_P, nseg, max_seg, STFT_NFFT, fs, pmax, 0, d_P, stream=stream)
+    else:
+        eng.stft_db_direct_device(slow, flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs, max_seg,
+                                  pmax, d_P, d_halo=hbuf, n_halo=n_halo, d_halo_len=hl, stream=stream)
 
 
 def sticky_check(eng, where: str) -> None:
@@ -447,11 +461,8 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     def step():
         eng.process_device(d_iq, F, FMCW_C32H, outs, d_rd=d_rd, out_dtype=FMCW_C32H, stream=stream)
         eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
-        pmax.zero_()
-        eng.stft_power_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
-                              max_seg, None, pmax, nseg, stream=stream)
-        eng.stft_db_direct_device(outs["slow_mag"], flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs,
-                                  max_seg, pmax, d_P, stream=stream)
+        stft_leg(eng, args.stft_form, outs["slow_mag"], flist, d_len, C, win, fs, max_seg, d_P, pmax, nseg,
+                 None, None, 0, None, stream)
 
     for _ in range(args.warmup):
         step()

@@ -29,13 +29,24 @@ namespace fmcw {
 // consecutive chirps.  Thread t loads samples t + T*m (coalesced), keeps them
 // in registers through the FFT and stores range bins t + T*m (coalesced).
 //
-// Streaming: the {cal, IF*w} taps sit in LDS (loaded once per workgroup) and
-// the twiddles of a chirp are loaded before the NEXT chirp's samples are
-// requested, so while chirp c is transformed the loads of chirp c+1 are in
-// flight (vmcnt completes in order: nothing issued after them is waited on).
+// Streaming: the {cal, IF*w} taps sit in LDS (loaded once per workgroup); three
+// workgroups per CU (3 waves per SIMD) keep loads in flight while other waves
+// transform (K1_PREFETCH: the round-3 form, the next chirp's samples requested
+// before this chirp's FFT, at 2 waves per SIMD).
 // ---------------------------------------------------------------------------
+// Occupancy over prefetch (config 2, 4096 frames, one box, 3 alternating rounds,
+// tools/gpu_k1ab.sh): no register prefetch at 3 waves per SIMD (<= 168 VGPRs) 824-827 us;
+// the round-3 register prefetch of the next chirp at 2 waves per SIMD 846-849 us; that
+// prefetch squeezed into 3 waves per SIMD spills (1637 us).  K1_PREFETCH=1 restores it (A/B).
+#ifndef K1_WAVES
+#ifdef K1_PREFETCH
+#define K1_WAVES 2
+#else
+#define K1_WAVES 3
+#endif
+#endif
 template <int NR, typename TIn, typename TCube, bool PROFILE>
-__global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
+__global__ __launch_bounds__(256, K1_WAVES) void k_range(RangeArgs a) {
   using Plan = FftPlan<NR>;
   constexpr int P = Plan::P, T = Plan::T;
   constexpr int TEAMS = T >= 256 ? 1 : 256 / T;
@@ -85,6 +96,15 @@ __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
     float2 tb[FftPasses<NR>::NB];
     load_tw_bases<NR>(tb, t, a.tw);                            // before the prefetch below
     const bool vn = (c + 1 < a.cpt) && (g + 1 < a.nchirps);
+#ifndef K1_PREFETCH   // the next chirp is loaded after this one's stores; the other waves of the SIMD cover it
+    chirp_finish<NR>(cur, in + (valid ? g : 0) * a.S, valid, out + g * NR, a.S, taps, a.cal_sum, a.cube_scale, tb,
+                     my, myred, t);
+    if constexpr (PROFILE) {
+#pragma unroll
+      for (int m = 0; m < P; ++m) pm[m] = fmaxf(pm[m], cabs2(cur[m]));
+    }
+    chirp_load<NR>(in + (vn ? g + 1 : 0) * a.S, vn, nmax, t, cur);
+#else
     float2 nxt[P];
     chirp_load<NR>(in + (vn ? g + 1 : 0) * a.S, vn, nmax, t, nxt);
     chirp_finish<NR>(cur, in + (valid ? g : 0) * a.S, valid, out + g * NR, a.S, taps, a.cal_sum, a.cube_scale, tb,
@@ -95,6 +115,7 @@ __global__ __launch_bounds__(256, 2) void k_range(RangeArgs a) {
     }
 #pragma unroll
     for (int m = 0; m < P; ++m) cur[m] = nxt[m];
+#endif
   }
   if constexpr (PROFILE) {
     if (g0 >= a.nchirps) return;                               // :210 max over chirps

@@ -9,6 +9,8 @@
 //                 interp1 onto 1024 logspace bins (table from the host)
 //   k_synth       SURVEY.md 8d synthetic frames (bench/test input only)
 #include "fft_team.h"
+
+#include <cstdlib>
 #include "fmcw_internal.h"
 #include "../../include/fmcw.h"
 
@@ -237,6 +239,103 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
   }
 }
 
+// ---------------------------------------------------------------------------
+// The nfft-64 case of k_stft20 MODE 0 / 1 (config 4's hop-1 Hann(20) STFT at nfft 64, 33
+// one-sided bins) on the matrix cores: per 16 segments, the [16 seg x 20 tap] window-sample
+// matrix (a Hankel matrix of the slow-time signal: row s = x[s .. s+19]) times the [20 x 64]
+// table of W[bin][m] = w[m] e^{-2 pi i bin m / 64}, as 4 x 5 v_mfma_f32_16x16x4_f32:
+//   tile 0: Re W of bins 0-15; tile 1: Im W of bins 1-15, column 0 = Re W of bin 32 (Nyquist:
+//   its Im W and bin 0's are exactly -0, so that column is free); tile 2 / 3: Re / Im W of
+//   bins 16-31.
+// An f32 MFMA is a k-ordered chain of f32 fmas (cdna_hip_programming.md, FP32-input MFMA), so
+// each S(seg, bin) is the same chain over m = 0..19 as k_stft20's v_pk_fma_f32 loop: P and
+// max(P) are bit-identical (tests/test_gpu_stft_mfma.py).  Lane l of a wave: A = x[seg_base +
+// (l & 15) + 4 q + (l >> 4)], B = its tile's W[col = l & 15][m = 4 q + (l >> 4)]; result
+// register r: segment seg_base + 4 (l >> 4) + r, column l & 15.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __restrict__ tab) {
+  constexpr int TS = 256;
+  typedef float f4t __attribute__((ext_vector_type(4)));
+  __shared__ float xs[TS * 4 + STFT_W];
+  __shared__ float bmax[4];
+  const int64_t L = *a.len;
+  const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
+  const int64_t Lx = L + H;
+  const int noverlap = STFT_W - a.hop;
+  int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
+  if (nseg > a.max_seg) nseg = a.max_seg;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+  const int64_t s0 = (int64_t)blockIdx.x * TS;
+  if (s0 >= nseg) return;                                           // block-uniform
+  const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
+  const int nsamp = (ns - 1) * a.hop + STFT_W;
+  const int64_t q0 = s0 * a.hop;
+  for (int i = threadIdx.x; i < TS * a.hop + STFT_W; i += 256) {    // zero past the last segment's samples
+    const int64_t q = q0 + i;
+    xs[i] = i >= nsamp ? 0.f : q < L ? a.slow_mag[(int64_t)a.frame_list[q / a.pn] * a.pn + (q % a.pn)] : a.halo[q - L];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
+  // the B operands of the 4 column tiles x 5 k-steps, and sum(w.^2) = sum |W[0][m]|^2
+  float bw[4][5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int m = 4 * q + kq;
+    bw[0][q] = tab[col * STFT_W + m].x;
+    bw[1][q] = col == 0 ? tab[32 * STFT_W + m].x : tab[col * STFT_W + m].y;
+    bw[2][q] = tab[(16 + col) * STFT_W + m].x;
+    bw[3][q] = tab[(16 + col) * STFT_W + m].y;
+  }
+  float u = 0.f;
+#pragma unroll
+  for (int m = 0; m < STFT_W; ++m) u = fmaf(tab[m].x, tab[m].x, u);
+  const float scale = a.inv_fs / u;                                 // 1/(fs*sum(w.^2))
+  __syncthreads();
+  float lmax = 0.f;
+  constexpr int NB = 33;
+#pragma unroll 1
+  for (int g = 0; g < 4; ++g) {                                     // 4 groups of 16 segments per wave
+    const int sb = w * 64 + 16 * g;
+    if (sb >= ns) break;                                            // wave-uniform
+    f4t acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const float av = xs[(sb + col) * a.hop + 4 * q + kq];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[t][q], acc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sl = sb + 4 * kq + r;
+      const bool ok = sl < ns;
+      const float re0 = acc[0][r], im0 = col == 0 ? 0.f : acc[1][r];
+      const float p0 = fmaf(re0, re0, im0 * im0) * scale * (col == 0 ? 1.f : 2.f);
+      const float re1 = acc[2][r], im1 = acc[3][r];
+      const float p1 = fmaf(re1, re1, im1 * im1) * scale * 2.f;
+      const float rn = acc[1][r];                                   // column 0: Re S of bin 32
+      const float pn = fmaf(rn, rn, 0.f * 0.f) * scale;
+      if (ok) {
+        lmax = fmaxf(lmax, fmaxf(p0, p1));
+        if (col == 0) lmax = fmaxf(lmax, pn);
+        if constexpr (MODE == 0) {
+          float* row = a.P + (s0 + sl) * NB;
+          row[col] = p0;
+          row[16 + col] = p1;
+          if (col == 0) row[32] = pn;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+  if (lane == 0) bmax[w] = lmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
+    atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+  }
+}
+
 __global__ __launch_bounds__(256) void k_stft_db(StftDbArgs a) {
   const int64_t nseg = *a.nseg;
   const float pm = *a.pmax;
@@ -257,6 +356,26 @@ __global__ __launch_bounds__(256) void k_stft_db(StftDbArgs a) {
       a.out[o] = d0 + w * (d1 - d0);                               // :299 interp1 'linear','extrap'
     }
   }
+}
+
+// :283 without resampling: P [nseg][nb] and the dB map are the same flat array shape, so the
+// map is one elementwise pass, 16 bytes per lane (P and out 16-byte aligned; may alias).
+__global__ __launch_bounds__(256) void k_stft_db_flat(StftDbArgs a) {
+  typedef float f4t __attribute__((ext_vector_type(4)));
+  const int64_t n = *a.nseg * a.nbins_in;
+  const float pm = *a.pmax;
+  const float inv = pm > 0.f ? 1.0f / pm : 0.f;
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const f4t* __restrict__ in = reinterpret_cast<const f4t*>(a.P);
+  f4t* out = reinterpret_cast<f4t*>(a.out);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f4t v = in[i];
+    out[i] = f4t{20.0f * log10f(v.x * inv), 20.0f * log10f(v.y * inv), 20.0f * log10f(v.z * inv),
+                 20.0f * log10f(v.w * inv)};
+  }
+  for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    a.out[i] = 20.0f * log10f(a.P[i] * inv);
 }
 
 // ---------------------------------------------------------------------------
@@ -361,6 +480,13 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
   if (ysplit < 1) ysplit = 1;
   const int col_chunk = (int)((chunks + ysplit - 1) / ysplit) * 32;
   const dim3 grid((unsigned)blocks, (unsigned)((ncol + col_chunk - 1) / col_chunk));
+  // nfft 64 (config 4): P / max(P) on the matrix cores, bit-identical (FMCW_STFT_MFMA=0: VALU)
+  const char* mf = std::getenv("FMCW_STFT_MFMA");
+  if (a.nfft == 64 && (mode == 0 || mode == 1) && !(mf && mf[0] == '0')) {
+    if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab);
+    else hipLaunchKernelGGL(k_stft64m<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab);
+    return hipGetLastError();
+  }
   if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
   else if (mode == 1) hipLaunchKernelGGL(k_stft20<1>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
   else if (mode == 2) hipLaunchKernelGGL(k_stft20<2>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
@@ -386,6 +512,11 @@ hipError_t launch_stft_power(const StftArgs& a, hipStream_t s) {
 hipError_t launch_stft_db(const StftDbArgs& a, hipStream_t s) {
   if (a.max_seg <= 0) return hipSuccess;
   const int nout = a.nlog > 0 ? a.nlog : a.nbins_in;
+  const bool aligned = ((reinterpret_cast<uintptr_t>(a.P) | reinterpret_cast<uintptr_t>(a.out)) & 15) == 0;
+  if (a.nlog == 0 && aligned) {
+    hipLaunchKernelGGL(k_stft_db_flat, dim3(grid_for(a.max_seg * nout, 16)), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_stft_db, dim3(grid_for(a.max_seg * nout, 4)), dim3(256), 0, s, a);
   return hipGetLastError();
 }

@@ -1,9 +1,8 @@
 // kernels_xcd.hip -- the XCD-team schedule of range + Doppler (k_rdx) for gfx950.
 //
-// The single pass (kernels_onepass.hip) splits a frame into 8 range tiles that
-// each re-read the whole 2 MiB frame from L2: 16 MiB of L2->CU traffic per
-// frame, which caps it near the L2 read ceiling.  Here the 32 CUs of one XCD
-// share a frame the way the reference computes it (radar_processing.m:199-219):
+// A config-3 frame (256 chirps x 1024 samples, 2 MiB) and its range cube do not fit one CU
+// (512 KiB of VGPRs + 160 KiB of LDS), so the 32 CUs of one XCD share a frame the way the
+// reference computes it (radar_processing.m:199-219):
 //
 //   range   (:203-205): member k transforms chirps 8k .. 8k+7, one per wave,
 //                       as a full 1024-point FFT, and writes its 1024 bins of
@@ -13,22 +12,23 @@
 //                       chirps, 64 KiB) back, takes the row means / maxima,
 //                       windows, runs 32 Doppler FFTs and writes its RD rows.
 //
-// So each input byte is read once, and the cube (2 MiB per frame) makes one
-// trip through the XCD instead of eight L2 re-reads of the frame.  One
-// persistent 512-thread workgroup per CU; the 32 blocks that land on XCD x
-// (HW_REG_XCC_ID; xcd_census checks the 32-per-XCD deal before the schedule is
-// enabled) form its team, members k = 0..31 by ticket, and take frames x + 8 j.
-// Step j publishes R(j-1), runs R(j) and D(j-2) (the Doppler two steps behind,
-// see the step loop); a ring of `slots` (4) slots per XCD with one ready
-// counter each: D(j-2) starts when all 32 members published frame j-2.
+// So each input byte is read once from HBM and the cube (2 MiB per frame) makes one trip
+// through the XCD's L2 (the retired 8-tile pass re-read the whole frame from L2 eight
+// times: DESIGN.md 4.1).  One persistent 512-thread workgroup per CU; the 32 blocks that
+// land on XCD x (HW_REG_XCC_ID; xcd_census checks the 32-per-XCD deal and the occupancy
+// before the schedule is enabled) form its team, members k = 0..31 by ticket, and take
+// frames x + 8 j.  Step j publishes R(j-1), runs R(j) and D(j-2) (the Doppler two steps
+// behind, see the step loop); a ring of kNS = 2 slots of 2 MiB per XCD with one ready counter
+// each: D(j-2) reads group k of frame j-2's slot once all 32 members published it.
 //
-// Hand-off protocol (tools/xcd_probe.hip measured it at 0.99 M frames/s of
-// pure data movement): producers store the slot with plain stores (the lines
-// stay in the XCD's L2), `s_waitcnt vmcnt` in every wave, a workgroup barrier,
-// then one agent-scope atomic add on the slot's ready counter.  Consumers poll
-// with relaxed agent loads (global_load sc1), then read the slot with
-// buffer_load sc1, which bypasses the CU's L1 and is served by the XCD's L2.
-// Producer and consumer are on the same XCD, so no L2 write-back is needed.
+// Hand-off protocol: producers store the slot with plain buffer stores (write-back in the
+// XCD's L2: a line rewritten while resident never leaves it, tools/r04_probe.hip part C; the
+// 2-slot ring competes with the input and RD lines, so about half its lines are written back
+// and re-read through the fabric), `s_waitcnt vmcnt` in every wave, a
+// workgroup barrier, then one agent-scope atomic add on the slot's ready counter.
+// Consumers poll with scalar loads that miss the scalar cache (s_load glc), then read the
+// slot with buffer_load sc1, which bypasses the CU's L1 and is served by the XCD's L2.
+// Producer and consumer are on the same XCD, so no L2 write-back is needed for visibility.
 // Every wait is bounded: a timeout sets xerr bit 0 and lets the grid drain.
 //
 // Reference chirp (static-target cancellation, :204 / :217-218).  Every chirp

@@ -133,12 +133,13 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
   f4v hold[NL];                                // HO == 0: the input handed to D directly (same member)
   auto body = [&](int j, bool dj, bool rj, bool pub, auto CNT, bool next) __attribute__((always_inline)) {
     if (pub) vm_wait<decltype(CNT)::value>();
-    if (HO && dj && tid < 64) wait_ge(&ready[((j - LAG) % NS) * 32], (unsigned)(NK * ((j - LAG) / NS + 1)), err + 1);
+    constexpr bool SYNC = HO == 1 || HO == 3, TRAF = HO == 1 || HO == 2;
+    if (SYNC && dj && tid < 64) wait_ge(&ready[((j - LAG) % NS) * 32], (unsigned)(NK * ((j - LAG) / NS + 1)), err + 1);
     if (pub || dj) __syncthreads();
-    if (HO && pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (SYNC && pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     f4v grp[NL];
     if (dj) {
-      if (HO) {
+      if (TRAF) {
         const char* g = slotp(j - LAG) + (long)k * UC * 256;
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, UC * 256, 0x00020000);
 #pragma unroll
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
       }
     }
     if (rj) {
-      if (HO) {
+      if (TRAF) {
         char* s = slotp(j);
         const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(s, (short)0, (int)UB, 0x00020000);
 #pragma unroll
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
         for (int i = 0; i < NL; ++i) hold[i] = xin[i];
       }
     }
-    if (HO) {
+    if (TRAF) {
       if (rj) vm_wait<NL>();
       else vm_wait<0>();
     }
@@ -186,6 +187,82 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
     for (int j = LAG + 1; j < nj; ++j) body(j, true, true, true, CS{}, true);
     body(nj, true, false, true, CS{}, false);
     for (int j = nj + 1; j < nj + LAG; ++j) body(j, true, false, false, C0{}, false);
+  }
+  if (acc.x == 1234.5f) rd[tid] = 1;
+}
+
+// k_rdx's own protocol with the group consumed one step after it is loaded: step j publishes
+// R(j-1) (after its slot stores completed), stores D(j-2)'s rows from the group loaded in step
+// j-1, polls ready(j-1) and loads group k of unit j-1, writes R(j)'s slot (after that poll: every
+// read of the slot's previous unit is done), then loads the next unit's input.  2 slots.
+template <int UC>
+__global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
+                                                     unsigned* ctr, long nunits, unsigned* err) {
+  constexpr int THR = 512, NS = 2;
+  constexpr long UB = (long)UC * NR * 8;
+  constexpr int NL = UC * 16 / THR;
+  __shared__ int team[2];
+  __shared__ unsigned gflag;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    team[0] = (int)xcc;
+    team[1] = (int)__hip_atomic_fetch_add(ctr + CTR_TICKET + xcc * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    gflag = 0;
+  }
+  __syncthreads();
+  const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
+  if (k >= NK) { atomicOr(err, 2u); return; }
+  const int nj = (int)((nunits - x + 7) / 8);
+  unsigned* ready = ctr + x * 8 * 32;
+  char* slots0 = cube + (long)x * NS * UB;
+  auto ld_in = [&](long j, f4v (&v)[NL]) __attribute__((always_inline)) {
+    const char* q = iq + (x + 8 * j) * UB + (long)k * (UC / 32) * NR * 8;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(q), (short)0, (UC / 32) * NR * 8, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NL; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 2);
+  };
+  f4v xin[NL], grp[NL], acc{0.f, 0.f, 0.f, 0.f};
+  if (nj > 0) ld_in(0, xin);
+  for (int j = 0; j < nj + 2; ++j) {
+    const bool pub = j >= 1 && j - 1 < nj, dj = j >= 2, gj = j >= 1 && j - 1 < nj, rj = j < nj;
+    if (pub) vm_wait<NL>();                       // R(j-1)'s slot stores; the next input loads may fly
+    else vm_wait<0>();
+    __syncthreads();
+    if (pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (dj) {                                     // D(j-2): rows from the group loaded in step j-1
+      const long f = x + 8L * (j - 2);
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)k * 32 * UC * 8, (short)0, 32 * UC * 8, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) __builtin_amdgcn_raw_buffer_store_b128(grp[i], rr, (tid + THR * i) * 16, 0, 2);
+      acc += grp[0];
+    }
+    if (gj) {                                     // poll ready(j-1), then load group k of unit j-1
+      if (tid < 64) {
+        wait_ge(&ready[((j - 1) % NS) * 32], (unsigned)(NK * ((j - 1) / NS + 1)), err + 1);
+        if (tid == 0) *reinterpret_cast<volatile unsigned*>(&gflag) = (unsigned)j;
+      } else {
+        while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
+      }
+      const char* g = slots0 + (long)((j - 1) % NS) * UB + (long)k * UC * 256;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, UC * 256, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) grp[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 16);
+    }
+    if (rj) {                                     // R(j): the slot (its previous unit was read by all: ready(j-1) seen)
+      if (j >= 1) vm_wait<NL>();                  // xin of unit j (the group loads may fly)
+      else vm_wait<0>();
+      char* s = slots0 + (long)(j % NS) * UB;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(s, (short)0, (int)UB, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int e = tid + THR * i, ch = k * (UC / 32) + (e >> 9), p = e & 511;
+        __builtin_amdgcn_raw_buffer_store_b128(xin[i], rs, (((p >> 4) * UC + ch) * 16 + (p & 15)) * 16, 0, 0);
+      }
+      if (j + 1 < nj) ld_in(j + 1, xin);
+    }
   }
   if (acc.x == 1234.5f) rd[tid] = 1;
 }
@@ -313,6 +390,32 @@ int main(int argc, char** argv) {
     rb("half unit, in nt, RD sc1, 3 slots", teamu(k_team<512, 0, 1, 2, 16, 128>, 3, 128));
     rb("quarter unit, in nt, RD sc1, 2 slots", teamu(k_team<512, 0, 1, 2, 16, 64>, 2, 64));
     rb("quarter unit, in nt, RD nt, 2 slots", teamu(k_team<512, 0, 1, 2, 2, 64>, 2, 64));
+  }
+  if (part == 0 || part == 5) {
+    printf("== part E: the hand-off split into its traffic and its synchronisation (frame unit, 2 slots)\n");
+    rb("full hand-off", teamu(k_team<512, 0, 1, 2, 2>, 2, 256));
+    rb("traffic only (no publish / poll)", teamu(k_team<512, 0, 2, 2, 2>, 2, 256));
+    rb("sync only (no slot stores / loads)", teamu(k_team<512, 0, 3, 2, 2>, 2, 256));
+    rb("no hand-off", teamu(k_team<512, 0, 0, 2, 2>, 2, 256));
+    rb("quarter: full", teamu(k_team<512, 0, 1, 2, 2, 64>, 2, 64));
+    rb("quarter: traffic only", teamu(k_team<512, 0, 2, 2, 2, 64>, 2, 64));
+    rb("quarter: sync only", teamu(k_team<512, 0, 3, 2, 2, 64>, 2, 64));
+    rb("quarter: no hand-off", teamu(k_team<512, 0, 0, 2, 2, 64>, 2, 64));
+  }
+  auto teamd = [&](auto kern, int UCv) {
+    return timeit([&] {
+      CK(hipMemsetAsync(ctr, 0, 4096 * 4));
+      hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const char*)iq, cube, rd, ctr, F * 256 / UCv, err);
+    }, 5);
+  };
+  if (part == 0 || part == 6) {
+    printf("== part F: k_rdx's protocol, group consumed one step after its loads (2 slots)\n");
+    rb("frame unit, deferred group", teamd(k_team_def<256>, 256));
+    rb("half unit, deferred group", teamd(k_team_def<128>, 128));
+    rb("quarter unit, deferred group", teamd(k_team_def<64>, 64));
+    rb("eighth unit, deferred group", teamd(k_team_def<32>, 32));
+    rb("(part B) frame unit, full", teamu(k_team<512, 0, 1, 2, 2>, 2, 256));
+    rb("(part B) no hand-off", teamu(k_team<512, 0, 0, 2, 2>, 2, 256));
   }
   if (part == 0 || part == 3) {
     printf("== part C: a region rewritten in place, 16-B stores (WRITE_SIZE per byte from the pmc pass)\n");
