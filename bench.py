@@ -63,8 +63,8 @@ def parse():
                          "all GPUs (65536 = the config-5 stream: 16 steps on 1 GPU, 2 on 8)")
     ap.add_argument("--stft-form", choices=["direct", "stored"], default="stored",
                     help="dB of the STFT leg: stored = pass 1 writes P and max(P), pass 2 turns P into dB in "
-                         "place (0.154 ms per step); direct = pass 1 max(P) only, pass 2 recomputes P and "
-                         "writes dB (0.171 ms; profiles/r04d_stft_ab.txt)")
+                         "place (0.103 ms per step); direct = pass 1 max(P) only, pass 2 recomputes P and writes "
+                         "dB, P never stored (0.124 ms; profiles/r04g_stft_ab.txt)")
     ap.add_argument("--dry-dist", action="store_true",
                     help="launcher test without a GPU: the ranks meet over gloo and rank 0 prints n_gpus")
     return ap.parse_args()

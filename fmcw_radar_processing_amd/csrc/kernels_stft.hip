@@ -16,6 +16,18 @@
 
 namespace fmcw {
 
+// max(P) of a block into the launch-wide maximum.  P >= 0, so the bit order of the floats is
+// their value order and an unsigned atomicMax combines them.  Thousands of blocks adding to ONE
+// word serialise at the memory side (~12 ns each, MI355X_MICROARCH.md fanin: ~44 us for the
+// 3,661 blocks of a config-4 step), so a block first reads the current maximum (an agent-scope
+// load, served by the L2) and skips the atomic when it cannot raise it; a stale read only costs
+// an unneeded atomic, never a wrong maximum.
+__device__ __forceinline__ void max_into(float* pmax, float m) {
+  unsigned* p = reinterpret_cast<unsigned*>(pmax);
+  const unsigned cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__float_as_uint(m) > cur) atomicMax(p, __float_as_uint(m));
+}
+
 // ---------------------------------------------------------------------------
 // exclusive scan of (count > 0) over F frames in one 1024-thread workgroup
 // ---------------------------------------------------------------------------
@@ -120,7 +132,7 @@ __global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
-    atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+    max_into(a.pmax, m);
   }
 }
 
@@ -234,13 +246,13 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
     __syncthreads();
     if (threadIdx.x == 0) {
       const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
-      atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+      max_into(a.pmax, m);
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// The nfft-64 case of k_stft20 MODE 0 / 1 (config 4's hop-1 Hann(20) STFT at nfft 64, 33
+// The nfft-64 case of k_stft20 MODE 0 / 1 / 2 (config 4's hop-1 Hann(20) STFT at nfft 64, 33
 // one-sided bins) on the matrix cores: per 16 segments, the [16 seg x 20 tap] window-sample
 // matrix (a Hankel matrix of the slow-time signal: row s = x[s .. s+19]) times the [20 x 64]
 // table of W[bin][m] = w[m] e^{-2 pi i bin m / 64}, as 4 x 5 v_mfma_f32_16x16x4_f32:
@@ -248,16 +260,18 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
 //   its Im W and bin 0's are exactly -0, so that column is free); tile 2 / 3: Re / Im W of
 //   bins 16-31.
 // An f32 MFMA is a k-ordered chain of f32 fmas (cdna_hip_programming.md, FP32-input MFMA), so
-// each S(seg, bin) is the same chain over m = 0..19 as k_stft20's v_pk_fma_f32 loop: P and
-// max(P) are bit-identical (tests/test_gpu_stft_mfma.py).  Lane l of a wave: A = x[seg_base +
+// each S(seg, bin) is the same chain over m = 0..19 as k_stft20's v_pk_fma_f32 loop: P, max(P)
+// and the direct dB are bit-identical (tests/test_gpu_stft_mfma.py).  The block's output (256
+// rows of 33 floats, contiguous) goes through LDS and leaves as 16-byte stores.  Lane l of a wave: A = x[seg_base +
 // (l & 15) + 4 q + (l >> 4)], B = its tile's W[col = l & 15][m = 4 q + (l >> 4)]; result
 // register r: segment seg_base + 4 (l >> 4) + r, column l & 15.
 // ---------------------------------------------------------------------------
 template <int MODE>
-__global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __restrict__ tab) {
-  constexpr int TS = 256;
+__global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __restrict__ tab, float* __restrict__ dst) {
+  constexpr int TS = 256, NB = 33;
   typedef float f4t __attribute__((ext_vector_type(4)));
   __shared__ float xs[TS * 4 + STFT_W];
+  __shared__ __attribute__((aligned(16))) float tile[MODE == 1 ? 4 : TS * NB];   // the block's [seg][bin] output
   __shared__ float bmax[4];
   const int64_t L = *a.len;
   const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
@@ -265,7 +279,7 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
   const int noverlap = STFT_W - a.hop;
   int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
   if (nseg > a.max_seg) nseg = a.max_seg;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+  if (MODE < 2 && blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
   const int64_t s0 = (int64_t)blockIdx.x * TS;
   if (s0 >= nseg) return;                                           // block-uniform
   const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
@@ -290,9 +304,17 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
 #pragma unroll
   for (int m = 0; m < STFT_W; ++m) u = fmaf(tab[m].x, tab[m].x, u);
   const float scale = a.inv_fs / u;                                 // 1/(fs*sum(w.^2))
+  float inv = 0.f;
+  if constexpr (MODE == 2) {
+    const float pm = *a.pmax;
+    inv = pm > 0.f ? 1.0f / pm : 0.f;                               // all-zero P: -Inf dB (MATLAB G = 0)
+  }
+  auto emit = [&](int sl, int b, float p) __attribute__((always_inline)) {
+    if constexpr (MODE == 0) tile[sl * NB + b] = p;
+    if constexpr (MODE == 2) tile[sl * NB + b] = 20.0f * log10f(p * inv);   // :283
+  };
   __syncthreads();
   float lmax = 0.f;
-  constexpr int NB = 33;
 #pragma unroll 1
   for (int g = 0; g < 4; ++g) {                                     // 4 groups of 16 segments per wave
     const int sb = w * 64 + 16 * g;
@@ -307,32 +329,160 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int sl = sb + 4 * kq + r;
-      const bool ok = sl < ns;
       const float re0 = acc[0][r], im0 = col == 0 ? 0.f : acc[1][r];
       const float p0 = fmaf(re0, re0, im0 * im0) * scale * (col == 0 ? 1.f : 2.f);
       const float re1 = acc[2][r], im1 = acc[3][r];
       const float p1 = fmaf(re1, re1, im1 * im1) * scale * 2.f;
       const float rn = acc[1][r];                                   // column 0: Re S of bin 32
       const float pn = fmaf(rn, rn, 0.f * 0.f) * scale;
-      if (ok) {
-        lmax = fmaxf(lmax, fmaxf(p0, p1));
-        if (col == 0) lmax = fmaxf(lmax, pn);
-        if constexpr (MODE == 0) {
-          float* row = a.P + (s0 + sl) * NB;
-          row[col] = p0;
-          row[16 + col] = p1;
-          if (col == 0) row[32] = pn;
+      if (sl < ns) {
+        if constexpr (MODE < 2) {
+          lmax = fmaxf(lmax, fmaxf(p0, p1));
+          if (col == 0) lmax = fmaxf(lmax, pn);
         }
+        emit(sl, col, p0);
+        emit(sl, 16 + col, p1);
+        if (col == 0) emit(sl, 32, pn);
       }
     }
   }
+  if constexpr (MODE != 1) {
+    // the block's rows s0 .. s0+ns-1 are one contiguous run of ns x 33 floats, 16-byte aligned
+    // (s0 x 33 x 4 = 33792 b): coalesced 16-byte stores
+    __syncthreads();
+    float* out = (MODE == 0 ? a.P : dst) + s0 * NB;
+    const int n = ns * NB, n4 = n >> 2;
+    const f4t* t4 = reinterpret_cast<const f4t*>(tile);
+    for (int i = threadIdx.x; i < n4; i += 256) reinterpret_cast<f4t*>(out)[i] = t4[i];
+    for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) out[i] = tile[i];
+  }
+  if constexpr (MODE < 2) {
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
-  if (lane == 0) bmax[w] = lmax;
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    if (lane == 0) bmax[w] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
+      max_into(a.pmax, m);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_stft20 on the matrix cores for any nfft (the host call's reference rule nfft =
+// 2^nextpow2(L), :273, e.g. 65536 for 256 config-3 frames): columns in chunks of 32 bins,
+// tiles 0 / 1 = Re / Im W of the chunk's bins 0-15, tiles 2 / 3 = bins 16-31, 5 k-steps of
+// v_mfma_f32_16x16x4_f32 per 16 segments and chunk.  MODE as k_stft20 (0 P + max, 1 max,
+// 2 dB, 3 P of the listed bins a.bins); the same k-ordered fma chain per output, so the
+// results are bit-identical to k_stft20's (tests/test_gpu_stft_mfma.py).
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __restrict__ tab, float* __restrict__ dst,
+                                                   int col_chunk) {
+  constexpr int TS = 256, KC = 32;
+  typedef float f4t __attribute__((ext_vector_type(4)));
+  __shared__ float xs[TS * 4 + STFT_W];
+  __shared__ float tile[MODE == 1 ? 4 : TS * (KC + 1)];
+  __shared__ float bmax[4];
+  const int64_t L = *a.len;
+  const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
+  const int64_t Lx = L + H;
+  const int noverlap = STFT_W - a.hop;
+  int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
+  if (nseg > a.max_seg) nseg = a.max_seg;
+  if (MODE < 2 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+  const int64_t s0 = (int64_t)blockIdx.x * TS;
+  if (s0 >= nseg) return;                                           // block-uniform
+  const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
+  const int nsamp = (ns - 1) * a.hop + STFT_W;
+  const int64_t q0 = s0 * a.hop;
+  for (int i = threadIdx.x; i < TS * a.hop + STFT_W; i += 256) {
+    const int64_t q = q0 + i;
+    xs[i] = i >= nsamp ? 0.f : q < L ? a.slow_mag[(int64_t)a.frame_list[q / a.pn] * a.pn + (q % a.pn)] : a.halo[q - L];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
+  float u = 0.f;
+#pragma unroll
+  for (int m = 0; m < STFT_W; ++m) u = fmaf(tab[m].x, tab[m].x, u);
+  const float scale = a.inv_fs / u;                                 // 1/(fs*sum(w.^2))
+  float inv = 0.f;
+  if constexpr (MODE == 2) {
+    const float pm = *a.pmax;
+    inv = pm > 0.f ? 1.0f / pm : 0.f;
+  }
+  const int nb = a.nfft / 2 + 1;
+  const int ncol = MODE == 3 ? a.ncol : nb;
+  const int c_lo = blockIdx.y * col_chunk;
+  const int c_hi = ncol - c_lo < col_chunk ? ncol : c_lo + col_chunk;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
-    atomicMax(reinterpret_cast<unsigned*>(a.pmax), __float_as_uint(m));   // P >= 0: bit order = value order
+  float lmax = 0.f;
+  for (int k0 = c_lo; k0 < c_hi; k0 += KC) {                        // uniform: columns k0 .. k0+KC-1
+    const int kn = c_hi - k0 < KC ? c_hi - k0 : KC;
+    // this lane's two columns of the chunk (col, 16 + col) and their bins
+    const bool v0 = col < kn, v1 = 16 + col < kn;
+    const int b0 = v0 ? (MODE == 3 ? a.bins[k0 + col] : k0 + col) : 0;
+    const int b1 = v1 ? (MODE == 3 ? a.bins[k0 + 16 + col] : k0 + 16 + col) : 0;
+    float bw[4][5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const int m = 4 * q + kq;
+      const float2 t0 = tab[(int64_t)b0 * STFT_W + m], t1 = tab[(int64_t)b1 * STFT_W + m];
+      bw[0][q] = v0 ? t0.x : 0.f;
+      bw[1][q] = v0 ? t0.y : 0.f;
+      bw[2][q] = v1 ? t1.x : 0.f;
+      bw[3][q] = v1 ? t1.y : 0.f;
+    }
+    const float g0 = (b0 == 0 || 2 * b0 == a.nfft) ? 1.f : 2.f;     // one-sided 'psd'
+    const float g1 = (b1 == 0 || 2 * b1 == a.nfft) ? 1.f : 2.f;
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {                                   // 4 groups of 16 segments per wave
+      const int sb = w * 64 + 16 * g;
+      if (sb >= ns) break;                                          // wave-uniform
+      f4t acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int q = 0; q < 5; ++q) {
+        const float av = xs[(sb + col) * a.hop + 4 * q + kq];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[t][q], acc[t], 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int sl = sb + 4 * kq + r;
+        const float p0 = fmaf(acc[0][r], acc[0][r], acc[1][r] * acc[1][r]) * scale * g0;
+        const float p1 = fmaf(acc[2][r], acc[2][r], acc[3][r] * acc[3][r]) * scale * g1;
+        if (sl < ns) {
+          if (v0) lmax = fmaxf(lmax, p0);
+          if (v1) lmax = fmaxf(lmax, p1);
+        }
+        if constexpr (MODE == 0 || MODE == 3) {
+          tile[sl * (KC + 1) + col] = p0;
+          tile[sl * (KC + 1) + 16 + col] = p1;
+        }
+        if constexpr (MODE == 2) {
+          tile[sl * (KC + 1) + col] = 20.0f * log10f(p0 * inv);
+          tile[sl * (KC + 1) + 16 + col] = 20.0f * log10f(p1 * inv);
+        }
+      }
+    }
+    if constexpr (MODE != 1) {
+      __syncthreads();
+      float* out = MODE == 0 ? a.P : dst;
+      for (int i = threadIdx.x; i < ns * kn; i += 256) {            // row-major [seg][col] chunk, coalesced per row
+        const int r = i / kn, c = i - r * kn;
+        out[(s0 + r) * ncol + k0 + c] = tile[r * (KC + 1) + c];
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (MODE < 2) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    if (lane == 0) bmax[w] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
+      max_into(a.pmax, m);
+    }
   }
 }
 
@@ -482,9 +632,18 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
   const dim3 grid((unsigned)blocks, (unsigned)((ncol + col_chunk - 1) / col_chunk));
   // nfft 64 (config 4): P / max(P) on the matrix cores, bit-identical (FMCW_STFT_MFMA=0: VALU)
   const char* mf = std::getenv("FMCW_STFT_MFMA");
-  if (a.nfft == 64 && (mode == 0 || mode == 1) && !(mf && mf[0] == '0')) {
-    if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab);
-    else hipLaunchKernelGGL(k_stft64m<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab);
+  const float* outp = mode == 0 ? a.P : dst;
+  if (a.nfft == 64 && mode <= 2 && !(mf && mf[0] == '0') && (mode == 1 || (reinterpret_cast<uintptr_t>(outp) & 15) == 0)) {
+    if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+    else if (mode == 1) hipLaunchKernelGGL(k_stft64m<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+    else hipLaunchKernelGGL(k_stft64m<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+    return hipGetLastError();
+  }
+  if (!(mf && mf[0] == '0')) {      // any other nfft: 32-bin column chunks on the matrix cores
+    if (mode == 0) hipLaunchKernelGGL(k_stft_mfma<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else if (mode == 1) hipLaunchKernelGGL(k_stft_mfma<1>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else if (mode == 2) hipLaunchKernelGGL(k_stft_mfma<2>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else hipLaunchKernelGGL(k_stft_mfma<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
     return hipGetLastError();
   }
   if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
