@@ -310,7 +310,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&iq, B));
   CK(hipMalloc(&rd, B));
   const long cube_bytes = 8L * 2 * 64 * UB;   // 8 XCDs x NS 2 x spread up to 64
-  CK(hipMalloc(&cube, cube_bytes));
+  // CUBE_ALLOC: 0 hipMalloc (coarse-grained, default), 1 fine-grained, 3 uncached (the hand-off
+  // ring's memory type: part G)
+  const int calloc_flag = getenv("CUBE_ALLOC") ? atoi(getenv("CUBE_ALLOC")) : 0;
+  if (calloc_flag) CK(hipExtMallocWithFlags((void**)&cube, cube_bytes, (unsigned)calloc_flag));
+  else CK(hipMalloc(&cube, cube_bytes));
   CK(hipMalloc(&ctr, 4096 * 4));
   CK(hipMalloc(&err, 8));
   CK(hipMalloc(&sink, 4096));
@@ -416,6 +420,12 @@ int main(int argc, char** argv) {
     rb("eighth unit, deferred group", teamd(k_team_def<32>, 32));
     rb("(part B) frame unit, full", teamu(k_team<512, 0, 1, 2, 2>, 2, 256));
     rb("(part B) no hand-off", teamu(k_team<512, 0, 0, 2, 2>, 2, 256));
+  }
+  if (part == 7) {
+    printf("== part G: the hand-off ring's memory type (CUBE_ALLOC=%d)\n", calloc_flag);
+    rb("frame unit, full (part B protocol)", teamu(k_team<512, 0, 1, 2, 2>, 2, 256));
+    rb("frame unit, deferred group (part F protocol)", teamd(k_team_def<256>, 256));
+    rb("half unit, deferred group", teamd(k_team_def<128>, 128));
   }
   if (part == 0 || part == 3) {
     printf("== part C: a region rewritten in place, 16-B stores (WRITE_SIZE per byte from the pmc pass)\n");
