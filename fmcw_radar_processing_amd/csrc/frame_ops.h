@@ -231,7 +231,9 @@ __device__ __forceinline__ void chirp_finish(float2 (&v)[FftPlan<NR>::P], const 
     const float2 d = make_float2(v[m].x - c.x - mu.x, v[m].y - c.y - mu.y);
     v[m] = n < nmax ? cscale(d, c.z) : make_float2(0.f, 0.f);
   }
+#ifndef K1_NOFFT     // diagnostic builds only (tools/ab_build.sh k1nofft -DK1_NOFFT): K1's data movement without its FFT
   team_fft_pre<NR>(v, my, t, tb, Sync{});                   // :205 fft(., Nr, 1)
+#endif
   if (valid) {
 #pragma unroll
     for (int m = 0; m < P; ++m) {                            // :207, write-once cube: `nt` stores

@@ -46,7 +46,7 @@ namespace fmcw {
 #endif
 #endif
 template <int NR, typename TIn, typename TCube, bool PROFILE>
-__global__ __launch_bounds__(256, K1_WAVES) void k_range(RangeArgs a) {
+__global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeArgs a) {   // Nr 2048: LDS allows 2
   using Plan = FftPlan<NR>;
   constexpr int P = Plan::P, T = Plan::T;
   constexpr int TEAMS = T >= 256 ? 1 : 256 / T;

@@ -82,6 +82,45 @@ __global__ __launch_bounds__(256) void k_write(f4v* __restrict__ o, long n) {
       if (base + 256L * u < n) __builtin_nontemporal_store(v, o + base + 256L * u);
 }
 
+// ---------------------------------------------------------------- part H: K1's access shape
+// config 2's K1 (k_range<512>) moves 4 KiB per chirp in and 4 KiB out: 32-thread teams, 8 per
+// 256-thread block, each team walking CPT chirps; lane t of a team holds elements t + 32 m
+// (m = 0..15, 8 bytes each).  W = 8: that shape, copied; W = 16: the same chirps as 8 loads of
+// 16 bytes per lane (elements 2t + 64 m', 2t + 1 + 64 m').  A data-movement ceiling for K1.
+template <int W, int CPT, int NT>
+__global__ __launch_bounds__(256, 3) void k_k1shape(const char* __restrict__ in, char* __restrict__ out, long nchirps) {
+  const int t = threadIdx.x & 31, team = threadIdx.x >> 5;
+  const long c0 = ((long)blockIdx.x * 8 + team) * CPT;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  for (int c = 0; c < CPT; ++c) {
+    const long ch = c0 + c;
+    if (ch >= nchirps) break;
+    if constexpr (W == 8) {
+      const f2* src = reinterpret_cast<const f2*>(in + ch * 4096);
+      f2* dst = reinterpret_cast<f2*>(out + ch * 4096);
+      f2 v[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) v[m] = NT ? __builtin_nontemporal_load(src + t + 32 * m) : src[t + 32 * m];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) {
+        if (NT) __builtin_nontemporal_store(v[m], dst + t + 32 * m);
+        else dst[t + 32 * m] = v[m];
+      }
+    } else {
+      const f4v* src = reinterpret_cast<const f4v*>(in + ch * 4096);
+      f4v* dst = reinterpret_cast<f4v*>(out + ch * 4096);
+      f4v v[8];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) v[m] = NT ? __builtin_nontemporal_load(src + t + 32 * m) : src[t + 32 * m];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        if (NT) __builtin_nontemporal_store(v[m], dst + t + 32 * m);
+        else dst[t + 32 * m] = v[m];
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------- part B: the hand-off
 __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
   unsigned v;
@@ -420,6 +459,19 @@ int main(int argc, char** argv) {
     rb("eighth unit, deferred group", teamd(k_team_def<32>, 32));
     rb("(part B) frame unit, full", teamu(k_team<512, 0, 1, 2, 2>, 2, 256));
     rb("(part B) no hand-off", teamu(k_team<512, 0, 0, 2, 2>, 2, 256));
+  }
+  if (part == 8) {
+    printf("== part H: K1's access shape (config 2: 524288 chirps of 4 KiB in and out; frac on K1's 4.30 GB)\n");
+    const long nch = 4096L * 128;
+    const double k1b = 4096.0 * 1050624 / 1e9;
+    auto rk = [&](const char* nm, float ms) { printf("%-40s %.3f ms  frac %.3f\n", nm, ms, k1b / ms / 8.0); };
+    rk("8-byte lanes, cpt 16, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<8, 16, 1>), dim3(nch / 128), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+    rk("16-byte lanes, cpt 16, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<16, 16, 1>), dim3(nch / 128), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+    rk("8-byte lanes, cpt 4, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<8, 4, 1>), dim3(nch / 32), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+    rk("16-byte lanes, cpt 4, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<16, 4, 1>), dim3(nch / 32), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+    rk("8-byte lanes, cpt 1, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<8, 1, 1>), dim3(nch / 8), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+    rk("16-byte lanes, cpt 1, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<16, 1, 1>), dim3(nch / 8), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+    rk("8-byte lanes, cpt 16, plain", timeit([&] { hipLaunchKernelGGL((k_k1shape<8, 16, 0>), dim3(nch / 128), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
   }
   if (part == 7) {
     printf("== part G: the hand-off ring's memory type (CUBE_ALLOC=%d)\n", calloc_flag);
