@@ -234,10 +234,13 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
 // R(j-1) (after its slot stores completed), stores D(j-2)'s rows from the group loaded in step
 // j-1, polls ready(j-1) and loads group k of unit j-1, writes R(j)'s slot (after that poll: every
 // read of the slot's previous unit is done), then loads the next unit's input.  2 slots.
-template <int UC>
+// LAGP: the unit polled and loaded in step j is j - LAGP (1: k_rdx); NS >= 2 LAGP slots (a member
+// that sees ready(j - LAGP) knows every member has read unit j - 2 LAGP)
+template <int UC, int LAGP = 1, int NS = 2>
 __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
                                                      unsigned* ctr, long nunits, unsigned* err) {
-  constexpr int THR = 512, NS = 2;
+  constexpr int THR = 512;
+  static_assert(NS >= 2 * LAGP && NS <= 8, "slot reuse: seeing ready(j - LAGP) proves unit j - 2 LAGP read");
   constexpr long UB = (long)UC * NR * 8;
   constexpr int NL = UC * 16 / THR;
   __shared__ int team[2];
@@ -265,32 +268,32 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
   };
   f4v xin[NL], grp[NL], acc{0.f, 0.f, 0.f, 0.f};
   if (nj > 0) ld_in(0, xin);
-  for (int j = 0; j < nj + 2; ++j) {
-    const bool pub = j >= 1 && j - 1 < nj, dj = j >= 2, gj = j >= 1 && j - 1 < nj, rj = j < nj;
+  for (int j = 0; j < nj + LAGP + 1; ++j) {
+    const bool pub = j >= 1 && j - 1 < nj, dj = j >= LAGP + 1, gj = j >= LAGP && j - LAGP < nj, rj = j < nj;
     if (pub) vm_wait<NL>();                       // R(j-1)'s slot stores; the next input loads may fly
     else vm_wait<0>();
     __syncthreads();
     if (pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (dj) {                                     // D(j-2): rows from the group loaded in step j-1
-      const long f = x + 8L * (j - 2);
+    if (dj) {                                     // D(j-1-LAGP): rows from the group loaded in step j-1
+      const long f = x + 8L * (j - 1 - LAGP);
       const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)k * 32 * UC * 8, (short)0, 32 * UC * 8, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NL; ++i) __builtin_amdgcn_raw_buffer_store_b128(grp[i], rr, (tid + THR * i) * 16, 0, 2);
       acc += grp[0];
     }
-    if (gj) {                                     // poll ready(j-1), then load group k of unit j-1
+    if (gj) {                                     // poll ready(j-LAGP), then load group k of unit j-LAGP
       if (tid < 64) {
-        wait_ge(&ready[((j - 1) % NS) * 32], (unsigned)(NK * ((j - 1) / NS + 1)), err + 1);
+        wait_ge(&ready[((j - LAGP) % NS) * 32], (unsigned)(NK * ((j - LAGP) / NS + 1)), err + 1);
         if (tid == 0) *reinterpret_cast<volatile unsigned*>(&gflag) = (unsigned)j;
       } else {
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }
-      const char* g = slots0 + (long)((j - 1) % NS) * UB + (long)k * UC * 256;
+      const char* g = slots0 + (long)((j - LAGP) % NS) * UB + (long)k * UC * 256;
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, UC * 256, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NL; ++i) grp[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 16);
     }
-    if (rj) {                                     // R(j): the slot (its previous unit was read by all: ready(j-1) seen)
+    if (rj) {                                     // R(j): the slot's previous unit j - NS <= j - 2 LAGP was read by all
       if (j >= 1) vm_wait<NL>();                  // xin of unit j (the group loads may fly)
       else vm_wait<0>();
       char* s = slots0 + (long)(j % NS) * UB;
@@ -472,6 +475,17 @@ int main(int argc, char** argv) {
     rk("8-byte lanes, cpt 1, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<8, 1, 1>), dim3(nch / 8), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
     rk("16-byte lanes, cpt 1, nt", timeit([&] { hipLaunchKernelGGL((k_k1shape<16, 1, 1>), dim3(nch / 8), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
     rk("8-byte lanes, cpt 16, plain", timeit([&] { hipLaunchKernelGGL((k_k1shape<8, 16, 0>), dim3(nch / 128), dim3(256), 0, 0, (const char*)iq, rd, nch); }));
+  }
+  if (part == 9) {
+    printf("== part I: k_rdx's protocol with a deeper poll lag (the unit polled was published LAGP steps earlier)\n");
+    rb("frame, lag 1, 2 slots (part F)", teamd(k_team_def<256, 1, 2>, 256));
+    rb("frame, lag 2, 4 slots", teamd(k_team_def<256, 2, 4>, 256));
+    rb("half, lag 1, 2 slots", teamd(k_team_def<128, 1, 2>, 128));
+    rb("half, lag 2, 4 slots", teamd(k_team_def<128, 2, 4>, 128));
+    rb("quarter, lag 2, 4 slots", teamd(k_team_def<64, 2, 4>, 64));
+    rb("quarter, lag 3, 6 slots", teamd(k_team_def<64, 3, 6>, 64));
+    rb("quarter, lag 4, 8 slots", teamd(k_team_def<64, 4, 8>, 64));
+    rb("eighth, lag 4, 8 slots", teamd(k_team_def<32, 4, 8>, 32));
   }
   if (part == 7) {
     printf("== part G: the hand-off ring's memory type (CUBE_ALLOC=%d)\n", calloc_flag);
