@@ -1005,6 +1005,7 @@ int fmcw_range_fft_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, i
   ra.cube_scale = out_dtype == FMCW_C32H ? 1.0f / p->nr : 1.0f;
   ra.profile = d_prof;
   int cpt = 16;
+  if (const char* e = std::getenv("FMCW_K1_CPT")) cpt = std::max(1, std::min(64, std::atoi(e)));   // A/B
   while (cpt > 1 && (p->pn % cpt) != 0) cpt >>= 1;
   ra.cpt = cpt;
   StageTimer tm(c, 6, s);

@@ -117,12 +117,47 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
     for (int m = 0; m < P; ++m) cur[m] = nxt[m];
 #endif
   }
-  if constexpr (PROFILE) {
-    if (g0 >= a.nchirps) return;                               // :210 max over chirps
-    const int64_t f = g0 / a.C;
-    unsigned* pb = reinterpret_cast<unsigned*>(a.profile) + f * NR;
+  if constexpr (PROFILE) {                                     // :210 max over chirps
+    constexpr bool kLdsCombine = Plan::STRIDE > 0 && (size_t)TEAMS * NR * 4 <= sizeof(lds);
+    if constexpr (kLdsCombine) {
+      // The block's teams combine their maxima in LDS (the FFT exchange region is free after the
+      // chirp loop): one plain store per (frame, bin) when the block's teams hold the whole frame
+      // (config 2: 8 teams x 16 chirps = 128), else one atomicMax per block and bin -- not one per
+      // team and bin (16.8 M atomics per config-2 launch).
+      __syncthreads();
+      float* pl = reinterpret_cast<float*>(lds);
 #pragma unroll
-    for (int m = 0; m < P; ++m) atomicMax(pb + t0 + T * m, __float_as_uint(sqrtf(pm[m])));
+      for (int m = 0; m < P; ++m) pl[team * NR + t0 + T * m] = pm[m];
+      __syncthreads();
+      const int64_t gb = (int64_t)blockIdx.x * TEAMS * a.cpt;   // the block's first chirp
+      for (int b = threadIdx.x; b < NR; b += 256) {
+        float acc = 0.f;
+        int64_t fcur = -1;
+        int nteam = 0;
+        for (int i = 0; i <= TEAMS; ++i) {
+          const int64_t gi = gb + (int64_t)i * a.cpt;
+          const bool vi = i < TEAMS && gi < a.nchirps;
+          const int64_t fi = vi ? gi / a.C : -2;
+          if (fi != fcur && fcur >= 0) {                      // flush the previous frame's group
+            float* dst = a.profile + fcur * NR + b;
+            if ((int64_t)nteam * a.cpt == a.C) *dst = sqrtf(acc);   // the whole frame: this block alone
+            else atomicMax(reinterpret_cast<unsigned*>(dst), __float_as_uint(sqrtf(acc)));
+            acc = 0.f;
+            nteam = 0;
+          }
+          if (!vi) break;
+          fcur = fi;
+          acc = fmaxf(acc, pl[i * NR + b]);
+          ++nteam;
+        }
+      }
+    } else {
+      if (g0 >= a.nchirps) return;
+      const int64_t f = g0 / a.C;
+      unsigned* pb = reinterpret_cast<unsigned*>(a.profile) + f * NR;
+#pragma unroll
+      for (int m = 0; m < P; ++m) atomicMax(pb + t0 + T * m, __float_as_uint(sqrtf(pm[m])));
+    }
   }
 }
 

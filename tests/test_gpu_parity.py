@@ -118,6 +118,25 @@ def test_range_fft_only(engine):
     assert rel_l2(prof, ref["profile"], axis=1).max() <= TOL_FP32_REL_L2
 
 
+@pytest.mark.parametrize("nts,pn,F,cpt", [(512, 128, 5, "4"), (512, 128, 3, "1"), (512, 48, 7, "16"),
+                                           (256, 40, 9, "8")])
+def test_range_fft_profile_block_combine(engine, monkeypatch, nts, pn, F, cpt):
+    """K1's :210 profile: the teams of a workgroup combine their maxima in LDS and store once per
+    (frame, bin) when they hold the whole frame, else add one atomicMax per workgroup -- with
+    workgroups that hold part of a frame (cpt 4, 1) or span frame boundaries (48 and 40 chirps
+    against 8 teams x cpt chirps)."""
+    monkeypatch.setenv("FMCW_K1_CPT", cpt)
+    cfg, p, wr, wd, cal = case(nts, pn, nts, 16, P.THROUGHPUT)
+    iq = O.synth_frames(F, pn, nts, nts, 16, p["dist_per_bin"], frame0=31)
+    engine.set_taps(cfg, cal, wr, wd)
+    cube, prof = engine.range_fft(iq)
+    ref = O.process_frames(iq, cal, p, wr, wd, want_cube=True)
+    assert rel_l2(cube, ref["cube"], axis=(1, 2)).max() <= TOL_FP32_REL_L2
+    assert rel_l2(prof, ref["profile"], axis=1).max() <= TOL_FP32_REL_L2
+    # the profile is the max over chirps of the cube's magnitudes (the same fp32 values)
+    np.testing.assert_allclose(prof, np.abs(cube).max(axis=1), rtol=1e-6)
+
+
 def test_deterministic(engine):
     cfg, p, wr, wd, cal = case(1024, 256, 1024, 256, P.THROUGHPUT)
     iq = O.synth_frames(2, 256, 1024, 1024, 256, p["dist_per_bin"])
