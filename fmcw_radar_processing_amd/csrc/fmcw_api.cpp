@@ -259,6 +259,7 @@ struct fmcw_ctx {
   int64_t chunk_frames = 0;
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
+  DevBuf k1_part;                               // K1's per-workgroup profile maxima (range-only calls)
   DevBuf x_cube, x_ctr, x_err, x_tab;          // XCD-team schedule: hand-off slots, counters, sticky error, XT_* table
   int xcd_teams = -1;                          // census of the device: its XCD teams (-1 not run yet, 0 none)
   int8_t xcc_team[16] = {};                    // HW_REG_XCC_ID -> team
@@ -1004,12 +1005,23 @@ int fmcw_range_fft_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, i
   ra.cube = d_cube; ra.cube_dtype = out_dtype;
   ra.cube_scale = out_dtype == FMCW_C32H ? 1.0f / p->nr : 1.0f;
   ra.profile = d_prof;
-  int cpt = 16;
+  int cpt = 8;      // config 2: 2 workgroups per frame (771-782 us vs 786-787 at 16; profiles/r04_k1_profile_combine.txt)
   if (const char* e = std::getenv("FMCW_K1_CPT")) cpt = std::max(1, std::min(64, std::atoi(e)));   // A/B
   while (cpt > 1 && (p->pn % cpt) != 0) cpt >>= 1;
   ra.cpt = cpt;
+  // workgroups of TEAMS teams x cpt chirps: when several share a frame evenly, their profile
+  // maxima go to per-workgroup slots (plain stores) and one reduction pass forms the profile
+  const int T = p->nr >= 16 ? p->nr / 16 : 1;
+  const int teams = T >= 256 ? 1 : 256 / T;
+  const int64_t per_wg = (int64_t)teams * cpt;
+  ra.parts = (per_wg < p->pn && p->pn % per_wg == 0) ? (int)(p->pn / per_wg) : 0;
+  if (ra.parts > 1) {
+    CHK(c->k1_part.ensure((size_t)F * ra.parts * p->nr * 4));
+    ra.prof_part = c->k1_part.as<float>();
+  }
   StageTimer tm(c, 6, s);
   HIPCHK(fmcw::launch_range(ra, s));
+  if (ra.parts > 1) HIPCHK(fmcw::launch_profile_reduce(ra.prof_part, ra.parts, F, p->nr, d_prof, s));
   tm.done();
   return FMCW_OK;
 }

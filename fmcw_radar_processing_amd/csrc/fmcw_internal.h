@@ -17,8 +17,10 @@ struct RangeArgs {
   void* cube;              // [nchirps][NR], dtype cube_dtype
   int cube_dtype;
   float cube_scale;        // stored value = X * cube_scale (1, or 1/NR for fp16)
-  float* profile;          // [frames][NR] (max over chirps, atomically raised) or nullptr
+  float* profile;          // [frames][NR] (max over chirps) or nullptr
   int cpt;                 // chirps per team (divides C when profile != nullptr)
+  float* prof_part;        // [frames][parts][NR] per-workgroup maxima when a workgroup holds 1/parts of
+  int parts;               // a frame (parts > 1), reduced by launch_profile_reduce; else nullptr / 0
 };
 
 struct DopplerArgs {
@@ -226,6 +228,8 @@ struct SynthArgs {
 };
 
 hipError_t launch_range(const RangeArgs& a, hipStream_t s);
+// profile[f][b] = max over parts of prof_part[f][part][b] (K1's per-workgroup maxima)
+hipError_t launch_profile_reduce(const float* part, int parts, int64_t frames, int nr, float* profile, hipStream_t s);
 hipError_t launch_doppler(const DopplerArgs& a, hipStream_t s);
 hipError_t launch_detect(const DetectArgs& a, hipStream_t s);
 hipError_t launch_compact(const int32_t* count, int64_t F, int pn, int32_t* frame_list, int64_t* len,

@@ -53,9 +53,11 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
   constexpr int LDSN = Plan::STRIDE > 0 ? Plan::STRIDE : 1;
   __shared__ float2 lds[TEAMS * LDSN];
   __shared__ float2 red[TEAMS * (T > 64 ? T / 64 : 1)];
-  __shared__ float4 taps[NR];
-
   const int nmax = a.S < NR ? a.S : NR;
+#ifdef K1_TAPS_GLOBAL   // A/B: taps read through the L1 from global memory (no per-workgroup LDS prologue)
+  const float4* taps = a.calw;
+#else
+  __shared__ float4 taps[NR];
   {
     constexpr int TP = (NR + 255) / 256;                       // taps per thread, loads issued together
     float4 tp[TP];
@@ -71,6 +73,7 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
     }
   }
   __syncthreads();
+#endif
 
   const int team = threadIdx.x / T, t0 = team_index<T>(threadIdx.x % T);   // bank-conflict-free LDS stores
   float2* my = lds + team * LDSN;
@@ -140,8 +143,17 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
           const int64_t fi = vi ? gi / a.C : -2;
           if (fi != fcur && fcur >= 0) {                      // flush the previous frame's group
             float* dst = a.profile + fcur * NR + b;
-            if ((int64_t)nteam * a.cpt == a.C) *dst = sqrtf(acc);   // the whole frame: this block alone
-            else atomicMax(reinterpret_cast<unsigned*>(dst), __float_as_uint(sqrtf(acc)));
+            const int64_t span = (int64_t)nteam * a.cpt;      // chirps of frame fcur in this block
+            if (span == a.C) {
+              *dst = sqrtf(acc);                              // the whole frame: this block alone
+            } else if (a.parts > 1 && span * a.parts == a.C) {
+              // one of the frame's `parts` equal workgroups: its maximum goes to its own slot
+              const int64_t g_start = gb + (int64_t)(i - nteam) * a.cpt;   // the group's first chirp
+              const int64_t part = (g_start - fcur * a.C) / span;
+              a.prof_part[(fcur * a.parts + part) * NR + b] = sqrtf(acc);
+            } else {
+              atomicMax(reinterpret_cast<unsigned*>(dst), __float_as_uint(sqrtf(acc)));
+            }
             acc = 0.f;
             nteam = 0;
           }
@@ -159,6 +171,29 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
       for (int m = 0; m < P; ++m) atomicMax(pb + t0 + T * m, __float_as_uint(sqrtf(pm[m])));
     }
   }
+}
+
+// profile[f][b] = max over K1's per-workgroup maxima of frame f (cpt chosen so that several
+// workgroups share a frame: plain stores there, this reduction instead of atomics)
+__global__ __launch_bounds__(256) void k_profile_reduce(const float* __restrict__ part, int parts, int64_t n, int nr,
+                                                        float* __restrict__ profile) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int64_t f = i / nr, b = i - f * nr;
+    const float* p = part + f * parts * (int64_t)nr + b;
+    float m = p[0];
+    for (int q = 1; q < parts; ++q) m = fmaxf(m, p[(int64_t)q * nr]);
+    profile[i] = m;
+  }
+}
+
+hipError_t launch_profile_reduce(const float* part, int parts, int64_t frames, int nr, float* profile, hipStream_t s) {
+  const int64_t n = frames * nr;
+  if (n <= 0) return hipSuccess;
+  int64_t b = (n + 1023) / 1024;
+  if (b > 65536) b = 65536;
+  hipLaunchKernelGGL(k_profile_reduce, dim3((unsigned)b), dim3(256), 0, s, part, parts, n, nr, profile);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -119,12 +119,13 @@ def test_range_fft_only(engine):
 
 
 @pytest.mark.parametrize("nts,pn,F,cpt", [(512, 128, 5, "4"), (512, 128, 3, "1"), (512, 48, 7, "16"),
-                                           (256, 40, 9, "8")])
+                                           (256, 40, 9, "8"), (512, 96, 4, "4"), (512, 128, 6, "8")])
 def test_range_fft_profile_block_combine(engine, monkeypatch, nts, pn, F, cpt):
     """K1's :210 profile: the teams of a workgroup combine their maxima in LDS and store once per
-    (frame, bin) when they hold the whole frame, else add one atomicMax per workgroup -- with
-    workgroups that hold part of a frame (cpt 4, 1) or span frame boundaries (48 and 40 chirps
-    against 8 teams x cpt chirps)."""
+    (frame, bin) when they hold the whole frame; workgroups that hold an equal part of a frame
+    (cpt 8, 4, 1: 2, 4 (3 at 96 chirps), 16 parts) store per-workgroup maxima that one reduction
+    pass combines; workgroups that span frame boundaries (48 and 40 chirps against 8 teams x cpt
+    chirps) add an atomicMax."""
     monkeypatch.setenv("FMCW_K1_CPT", cpt)
     cfg, p, wr, wd, cal = case(nts, pn, nts, 16, P.THROUGHPUT)
     iq = O.synth_frames(F, pn, nts, nts, 16, p["dist_per_bin"], frame0=31)
