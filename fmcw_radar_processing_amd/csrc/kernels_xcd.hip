@@ -108,9 +108,14 @@ struct LdsX {
 // the L2, where the agent-scope adds land).  It counts on lgkmcnt, not vmcnt, so the
 // polling wave's vector loads and stores stay in flight (a vector poll, or a call, would
 // make it wait for all of them first).  The value is waited for inside the asm.
+// (The address goes through readfirstlane, a no-op for a value already in SGPRs: a loop-invariant
+// counter address may otherwise be kept in VGPRs, which the "s" constraint cannot take.)
 __device__ __forceinline__ unsigned ld_flag(const unsigned* p) {
+  const unsigned long long u = reinterpret_cast<unsigned long long>(p);
+  const unsigned long long su = ((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(u >> 32)) << 32) |
+                                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)u);
   unsigned v;
-  asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(p) : "memory");
+  asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(reinterpret_cast<const unsigned*>(su)) : "memory");
   return v;
 }
 // Bounded wait for *p >= v (wave-uniform).  ~1 s before giving up; once any wait of
@@ -124,9 +129,10 @@ __device__ __forceinline__ void wait_ge(const unsigned* p, unsigned v, unsigned*
     if ((it & 63) == 63 && ld_flag(abort)) return;
     __builtin_amdgcn_s_sleep(2);
   }
-  if (threadIdx.x == 0) {
-    atomicOr(abort, 1u);
-    atomicOr(err, 1u);
+  if (threadIdx.x == 0) {   // global atomics (a flat atomic here tripped an LLVM aperture-check bug)
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    __hip_atomic_fetch_or((gu32*)abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_or((gu32*)err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
@@ -209,6 +215,9 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const int nj = a.F > x ? (int)((a.F - x + T - 1) / T) : 0;
   const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
   unsigned* ready = a.xctr + (x * 2 + 0) * 32 * XCD_MAX_SLOTS;
+#ifdef XK_DONE
+  unsigned* done = ready + 32 * XCD_MAX_SLOTS;
+#endif
 
   using TP = std::conditional_t<H, h4v, f4v>;
   const TP* __restrict__ iq = reinterpret_cast<const TP*>(a.iq);
@@ -565,7 +574,11 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   };
 
   char* __restrict__ slots0 = reinterpret_cast<char*>(a.xcube) + (int64_t)x * NS * kSlotBytes;
+#ifdef XK_DONE       // A/B: one slot per XCD, its reuse proven by a done counter (tools/r04_probe.hip part J)
+  auto slot = [&](int) __attribute__((always_inline)) { return slots0; };
+#else
   auto slot = [&](int j) __attribute__((always_inline)) { return slots0 + (int64_t)(j % kNS) * kSlotBytes; };
+#endif
   auto frame = [&](int j) __attribute__((always_inline)) { return x + (int64_t)T * j; };
   TP xin[8];
   f4v grp[8];
@@ -660,6 +673,19 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       c2 q0[8], q1[8];
       r_mid(u);
       r_t2(u, q0, q1);
+#ifdef XK_DONE
+      // one slot: every member's group loads of frame j - 1 (issued above) must have returned
+      // before R(j) rewrites it.  Count them out (done), then wait for the whole team.
+      if (gj) {
+        vm_wait<0>();
+        __syncthreads();
+        if (w == 0) {
+          if (lane == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          wait_ge(done, (unsigned)(NK * j), a.xctr + XCD_ABORT, a.xerr);
+        }
+        __syncthreads();
+      }
+#endif
       r_end(q0, q1, slot(j));
     }
     stamp(8);

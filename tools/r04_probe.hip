@@ -309,6 +309,87 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
   if (acc.x == 1234.5f) rd[tid] = 1;
 }
 
+// Part J: slot reuse proven by done counters instead of a later ready counter.  Step j: wait
+// until every member has read the slot's previous unit (done(j - NS)), store R(j), publish
+// ready(j); store D's RD rows of the group loaded in step j - 1; poll ready(j - NS + 1), load group
+// k of that unit, wait for the loads, publish done.  NS = 1: the unit is written and read in the
+// same step, so a slot line lives one step (2 MiB of ring per XCD at the frame unit) at the price
+// of a serial store -> ready -> load -> done chain per step.
+constexpr int CTR_DONE = 4096;                // [8 XCC][8 slots][32] done counters
+template <int UC, int NS>
+__global__ __launch_bounds__(512, 1) void k_team_done(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
+                                                      unsigned* ctr, long nunits, unsigned* err) {
+  constexpr int THR = 512, LAGD = NS - 1;
+  constexpr long UB = (long)UC * NR * 8;
+  constexpr int NL = UC * 16 / THR;
+  __shared__ int team[2];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    team[0] = (int)xcc;
+    team[1] = (int)__hip_atomic_fetch_add(ctr + CTR_TICKET + xcc * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
+  if (k >= NK) { atomicOr(err, 2u); return; }
+  const int nj = (int)((nunits - x + 7) / 8);
+  unsigned* ready = ctr + x * 8 * 32;
+  unsigned* done = ctr + CTR_DONE + x * 8 * 32;
+  char* slots0 = cube + (long)x * NS * UB;
+  auto ld_in = [&](long j, f4v (&v)[NL]) __attribute__((always_inline)) {
+    const char* q = iq + (x + 8 * j) * UB + (long)k * (UC / 32) * NR * 8;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(q), (short)0, (UC / 32) * NR * 8, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < NL; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 2);
+  };
+  f4v xin[NL], grp[NL], acc{0.f, 0.f, 0.f, 0.f};
+  if (nj > 0) ld_in(0, xin);
+  for (int j = 0; j < nj + LAGD + 1; ++j) {
+    if (j < nj) {
+      if (j >= NS && tid < 64) wait_ge(&done[(j % NS) * 32], (unsigned)(NK * ((j - NS) / NS + 1)), err + 1);
+      vm_wait<0>();                               // xin of unit j
+      __syncthreads();
+      char* s = slots0 + (long)(j % NS) * UB;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(s, (short)0, (int)UB, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int e = tid + THR * i, ch = k * (UC / 32) + (e >> 9), p = e & 511;
+        __builtin_amdgcn_raw_buffer_store_b128(xin[i], rs, (((p >> 4) * UC + ch) * 16 + (p & 15)) * 16, 0, 0);
+      }
+      if (j + 1 < nj) {
+        ld_in(j + 1, xin);
+        vm_wait<NL>();                            // the slot stores (the next input may fly)
+      } else {
+        vm_wait<0>();
+      }
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(&ready[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (j >= 1 && j - 1 - LAGD >= 0 && j - 1 - LAGD < nj) {   // D(u'): rows of the group loaded in step j - 1
+      const long f = x + 8L * (j - 1 - LAGD);
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)k * 32 * UC * 8, (short)0, 32 * UC * 8, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) __builtin_amdgcn_raw_buffer_store_b128(grp[i], rr, (tid + THR * i) * 16, 0, 2);
+      acc += grp[0];
+    }
+    const int u = j - LAGD;
+    if (u >= 0 && u < nj) {
+      if (tid < 64) wait_ge(&ready[(u % NS) * 32], (unsigned)(NK * (u / NS + 1)), err + 1);
+      __syncthreads();
+      const char* g = slots0 + (long)(u % NS) * UB + (long)k * UC * 256;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, UC * 256, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) grp[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 16);
+      vm_wait<0>();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(&done[(u % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (acc.x == 1234.5f) rd[tid] = 1;
+}
+
 // ---------------------------------------------------------------- part C: stores leaving the L2
 // every CU rewrites its own R-byte region `passes` times with policy AUX (16-byte stores);
 // WRITE_SIZE / bytes stored says whether each pass leaves the XCD's L2
@@ -357,7 +438,7 @@ int main(int argc, char** argv) {
   const int calloc_flag = getenv("CUBE_ALLOC") ? atoi(getenv("CUBE_ALLOC")) : 0;
   if (calloc_flag) CK(hipExtMallocWithFlags((void**)&cube, cube_bytes, (unsigned)calloc_flag));
   else CK(hipMalloc(&cube, cube_bytes));
-  CK(hipMalloc(&ctr, 4096 * 4));
+  CK(hipMalloc(&ctr, 8192 * 4));
   CK(hipMalloc(&err, 8));
   CK(hipMalloc(&sink, 4096));
   CK(hipMemset(err, 0, 8));
@@ -486,6 +567,23 @@ int main(int argc, char** argv) {
     rb("quarter, lag 3, 6 slots", teamd(k_team_def<64, 3, 6>, 64));
     rb("quarter, lag 4, 8 slots", teamd(k_team_def<64, 4, 8>, 64));
     rb("eighth, lag 4, 8 slots", teamd(k_team_def<32, 4, 8>, 32));
+  }
+  auto teamx = [&](auto kern, int UCv) {
+    return timeit([&] {
+      CK(hipMemsetAsync(ctr, 0, 8192 * 4));
+      hipLaunchKernelGGL(kern, dim3(256), dim3(512), 0, 0, (const char*)iq, cube, rd, ctr, F * 256 / UCv, err);
+    }, 5);
+  };
+  if (part == 10) {
+    printf("== part J: slot reuse by done counters (NS slots; NS = 1: written and read in one step)\n");
+    rb("frame, lag 1, 2 slots (part F)", teamd(k_team_def<256, 1, 2>, 256));
+    rb("frame, done, 1 slot", teamx(k_team_done<256, 1>, 256));
+    rb("frame, done, 2 slots", teamx(k_team_done<256, 2>, 256));
+    rb("half, done, 1 slot", teamx(k_team_done<128, 1>, 128));
+    rb("half, done, 2 slots", teamx(k_team_done<128, 2>, 128));
+    rb("half, done, 3 slots", teamx(k_team_done<128, 3>, 128));
+    rb("quarter, done, 2 slots", teamx(k_team_done<64, 2>, 64));
+    rb("quarter, done, 4 slots", teamx(k_team_done<64, 4>, 64));
   }
   if (part == 7) {
     printf("== part G: the hand-off ring's memory type (CUBE_ALLOC=%d)\n", calloc_flag);
