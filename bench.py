@@ -173,7 +173,10 @@ def main():
     if args.chunk:
         eng.set_chunk_frames(args.chunk)
     eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3, "xcd": 4}[args.pipeline])
-    stream = torch.cuda.current_stream(dev)
+    # one non-default stream for the engine's calls and torch's own work of the step (pmax.zero_,
+    # the RCCL collectives): ordered on one queue, no per-call side-stream joins (engine._sided)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
 
     # ---- device-resident input + outputs ------------------------------------------
     d_iq = torch.empty((F, C, S, 2), dtype=tdt, device=dev)

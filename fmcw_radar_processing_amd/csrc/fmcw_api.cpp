@@ -378,7 +378,10 @@ int check_ctx(fmcw_ctx* c, const fmcw_params* p) {
   if (p->nts != c->p.nts || p->pn != c->p.pn || p->nr != c->p.nr || p->nd != c->p.nd)
     return fail(FMCW_E_STATE, "nts/pn/nr/nd differ from the ones given to fmcw_set_taps");
   CHK(set_device(c));
-  if (p->if_scale != c->calw_scale) CHK(build_calw(c, p->if_scale, c->stream));
+  if (p->if_scale != c->calw_scale) {   // queued work on any stream may still read the old table
+    HIPCHK(hipDeviceSynchronize());
+    CHK(build_calw(c, p->if_scale, c->stream));
+  }
   return FMCW_OK;
 }
 
@@ -572,6 +575,10 @@ int fmcw_set_taps(fmcw_ctx* c, const fmcw_params* p, const float* range_win, con
   if (!range_win || !doppler_win || !calib) return fail(FMCW_E_ARG, "taps pointer is NULL");
   CHK(set_device(c));
   hipStream_t s = c->stream;
+  // the taps are read by work on the caller's streams, which the context's stream does not
+  // order against: let queued work finish with the old taps, and finish the copies before
+  // returning, so that a call on any stream afterwards reads the new ones
+  HIPCHK(hipDeviceSynchronize());
   CHK(c->wd.ensure((size_t)p->pn * 4));
   CHK(c->cal.ensure((size_t)p->nts * 8));
   HIPCHK(hipMemcpyAsync(c->wd.p, doppler_win, (size_t)p->pn * 4, hipMemcpyHostToDevice, s));
@@ -587,6 +594,7 @@ int fmcw_set_taps(fmcw_ctx* c, const fmcw_params* p, const float* range_win, con
   c->p = *p;
   c->taps = true;
   c->x_tab_ok = false;
+  HIPCHK(hipStreamSynchronize(s));
   for (fmcw_ctx* q : c->peers) CHK(fmcw_set_taps(q, p, range_win, doppler_win, calib));
   return FMCW_OK;
 }

@@ -10,6 +10,7 @@ Two call styles, both straight through the C-ABI of include/fmcw.h:
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as ct
 
 import numpy as np
@@ -169,57 +170,65 @@ class Engine:
 
     def render_spectrogram_device(self, d_Q, nq: int, d_nseg, d_pmax, nfft: int, fs: float, t0: float, dt: float,
                                   width: int, height: int, d_img, stream=None) -> None:
-        check(self.lib.fmcw_render_spectrogram_device(self.h, _ptr(d_Q), int(nq), _ptr(d_nseg), _ptr(d_pmax),
-                                                      int(nfft), float(fs), float(t0), float(dt), int(width),
-                                                      int(height), _ptr(d_img), _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_render_spectrogram_device(self.h, _ptr(d_Q), int(nq), _ptr(d_nseg), _ptr(d_pmax),
+                                                          int(nfft), float(fs), float(t0), float(dt), int(width),
+                                                          int(height), _ptr(d_img), hs))
 
     # ---- device API (torch tensors as HBM buffers) -------------------------------
     def process_device(self, d_iq, F: int, in_dtype: int, outs: dict, d_cube=None, d_rd=None,
                        out_dtype: int = FMCW_C64, probe_column: int = 0, stream=None) -> None:
         self._need()
-        check(self.lib.fmcw_process_device(
-            self.h, ct.byref(self.p), _ptr(d_iq), in_dtype, int(F), _ptr(outs["profile"]),
-            _ptr(outs["tgt_count"]), _ptr(outs["tgt_range_idx"]), _ptr(outs["tgt_range_mag"]),
-            _ptr(outs["tgt_doppler_idx"]), _ptr(outs["slow_mag"]), _ptr(d_cube), _ptr(d_rd), out_dtype,
-            int(probe_column), _ptr(outs.get("probe_mag")), _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_process_device(
+                self.h, ct.byref(self.p), _ptr(d_iq), in_dtype, int(F), _ptr(outs["profile"]),
+                _ptr(outs["tgt_count"]), _ptr(outs["tgt_range_idx"]), _ptr(outs["tgt_range_mag"]),
+                _ptr(outs["tgt_doppler_idx"]), _ptr(outs["slow_mag"]), _ptr(d_cube), _ptr(d_rd), out_dtype,
+                int(probe_column), _ptr(outs.get("probe_mag")), hs))
 
     def range_fft_device(self, d_iq, F: int, in_dtype: int, d_cube, d_prof, out_dtype: int = FMCW_C64,
                          stream=None) -> None:
         self._need()
-        check(self.lib.fmcw_range_fft_device(self.h, ct.byref(self.p), _ptr(d_iq), in_dtype, int(F), _ptr(d_cube),
-                                             out_dtype, _ptr(d_prof), _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_range_fft_device(self.h, ct.byref(self.p), _ptr(d_iq), in_dtype, int(F), _ptr(d_cube),
+                                                 out_dtype, _ptr(d_prof), hs))
 
     def compact_device(self, d_count, F: int, d_list, d_len, stream=None) -> None:
         cfg = self._need()
-        check(self.lib.fmcw_compact_device(self.h, _ptr(d_count), int(F), cfg.pn, _ptr(d_list), _ptr(d_len),
-                                           _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_compact_device(self.h, _ptr(d_count), int(F), cfg.pn, _ptr(d_list), _ptr(d_len),
+                                               hs))
 
     def stft_power_device(self, d_slow, d_list, d_len, pn: int, d_win, wlen: int, noverlap: int, nfft: int,
                           fs: float, max_seg: int, d_P, d_pmax, d_nseg, d_halo=None, n_halo: int = 0,
                           d_halo_len=None, stream=None) -> None:
-        check(self.lib.fmcw_stft_power_device(self.h, _ptr(d_slow), _ptr(d_list), _ptr(d_len), int(pn),
-                                              _ptr(d_halo), int(n_halo), _ptr(d_halo_len), _ptr(d_win),
-                                              int(wlen), int(noverlap),
-                                              int(nfft), float(fs), int(max_seg), _ptr(d_P), _ptr(d_pmax),
-                                              _ptr(d_nseg), _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_stft_power_device(self.h, _ptr(d_slow), _ptr(d_list), _ptr(d_len), int(pn),
+                                                  _ptr(d_halo), int(n_halo), _ptr(d_halo_len), _ptr(d_win),
+                                                  int(wlen), int(noverlap),
+                                                  int(nfft), float(fs), int(max_seg), _ptr(d_P), _ptr(d_pmax),
+                                                  _ptr(d_nseg), hs))
 
     def stft_db_direct_device(self, d_slow, d_list, d_len, pn: int, d_win, wlen: int, noverlap: int, nfft: int,
                               fs: float, max_seg: int, d_pmax, d_out, d_halo=None, n_halo: int = 0, d_halo_len=None,
                               stream=None) -> None:
-        check(self.lib.fmcw_stft_db_direct_device(self.h, _ptr(d_slow), _ptr(d_list), _ptr(d_len), int(pn),
-                                                  _ptr(d_halo), int(n_halo), _ptr(d_halo_len), _ptr(d_win),
-                                                  int(wlen), int(noverlap), int(nfft), float(fs), int(max_seg),
-                                                  _ptr(d_pmax), _ptr(d_out), _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_stft_db_direct_device(self.h, _ptr(d_slow), _ptr(d_list), _ptr(d_len), int(pn),
+                                                      _ptr(d_halo), int(n_halo), _ptr(d_halo_len), _ptr(d_win),
+                                                      int(wlen), int(noverlap), int(nfft), float(fs), int(max_seg),
+                                                      _ptr(d_pmax), _ptr(d_out), hs))
 
     def stft_db_device(self, d_P, d_nseg, max_seg: int, nfft: int, fs: float, d_pmax, n_log_bins: int, d_out,
                        stream=None) -> None:
-        check(self.lib.fmcw_stft_db_device(self.h, _ptr(d_P), _ptr(d_nseg), int(max_seg), int(nfft), float(fs),
-                                           _ptr(d_pmax), int(n_log_bins), _ptr(d_out), _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_stft_db_device(self.h, _ptr(d_P), _ptr(d_nseg), int(max_seg), int(nfft), float(fs),
+                                               _ptr(d_pmax), int(n_log_bins), _ptr(d_out), hs))
 
     def synth_device(self, d_iq, frame0: int, F: int, dtype: int = FMCW_C64, stream=None) -> None:
         self._need()
-        check(self.lib.fmcw_synth_device(self.h, ct.byref(self.p), int(frame0), int(F), _ptr(d_iq), dtype,
-                                         _stream(stream)))
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_synth_device(self.h, ct.byref(self.p), int(frame0), int(F), _ptr(d_iq), dtype,
+                                             hs))
 
     # ---- timing -----------------------------------------------------------------
     def timing(self, level: int) -> None:
@@ -247,11 +256,37 @@ class Engine:
 
 
 def _stream(stream) -> ct.c_void_p:
+    """The hipStream_t of a call: None = the context's own stream (include/fmcw.h: NULL), an int
+    = a raw handle, a torch.cuda.Stream = its handle (see _sided for torch's default stream)."""
     if stream is None:
         return ct.c_void_p(0)
     if isinstance(stream, int):
         return ct.c_void_p(stream)
     return ct.c_void_p(int(stream.cuda_stream))   # torch.cuda.Stream
+
+
+_SIDE = {}
+
+
+@contextlib.contextmanager
+def _sided(stream):
+    """The stream handle for a device call on `stream`.  torch's default stream has handle 0,
+    which the C-ABI reads as the context's own (non-blocking) stream -- one that does not wait
+    for the torch work queued before the call (a flip, a mul_, an RCCL collective) nor the torch
+    work after it for the call.  So a call on torch's default stream runs on a side stream that
+    waits for it first and that it waits for afterwards: ordered like any torch kernel."""
+    if stream is None or isinstance(stream, int) or int(stream.cuda_stream) != 0:
+        yield _stream(stream)
+        return
+    import torch
+    side = _SIDE.get(stream.device)
+    if side is None:
+        side = _SIDE[stream.device] = torch.cuda.Stream(device=stream.device)
+    side.wait_stream(stream)
+    try:
+        yield ct.c_void_p(int(side.cuda_stream))
+    finally:
+        stream.wait_stream(side)
 
 
 def device_count() -> int:

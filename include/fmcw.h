@@ -117,7 +117,9 @@ int fmcw_ctx_devices(fmcw_ctx* ctx, int32_t* n_devices, int32_t* device_ids, int
  *   doppler_win [pn]         = 2*chebwin(PN)
  *   calib       [nts] c64    = calib_rx1
  * Also builds the twiddle tables for nr and nd.  Must precede processing and
- * be repeated whenever nts/pn/nr/nd change. */
+ * be repeated whenever nts/pn/nr/nd change.  Synchronous with the device: work
+ * queued before it (on any stream) finishes with the old taps, and calls after it
+ * (on any stream) see the new ones. */
 int fmcw_set_taps(fmcw_ctx* ctx, const fmcw_params* p, const float* range_win,
                   const float* doppler_win, const float* calib);
 

@@ -1,0 +1,145 @@
+"""GPU: BASELINE config 4 at its full size (4096 frames of 256 chirps x 1024 samples, 8.6 GB
+in HBM), checked through properties that do not need the oracle to run at that size
+(radar_processing.m:197-299 computes every frame on its own, and every step of it is linear):
+
+  * determinism: two runs give bit-identical outputs (RD map, profile, detections, slow-time
+    rows, the STFT dB map of the compacted rows);
+  * frame independence: the frames in reverse order give the reversed outputs bit for bit --
+    every frame lands on another XCD team, member and hand-off slot than before, so no state
+    leaks between frames through the slot ring;
+  * exact scaling: IQ and calibration times 2 give RD map and profile times 2 bit for bit
+    (every operation of the path commutes with a power-of-two scale: the conditioning, both
+    FFTs, the windows, the means, |.| and the square root), and the spectrogram's dB map --
+    normalised by its max(P), :283 -- of the slow-time rows times 2 is the same bit for bit.
+
+bench.py compares every frame of the same workload with the fp64 C oracle; these tests hold the
+path to the properties on every run of the GPU suite, for both storage formats.
+"""
+import numpy as np
+import pytest
+
+from fmcw_radar_processing_amd import FMCW_C32H, FMCW_C64, FMCW_PIPE_AUTO, FMCW_PIPE_XCD
+from fmcw_radar_processing_amd import params as P
+
+pytestmark = pytest.mark.gpu
+
+F = 4096
+WLEN, NOVERLAP, NFFT = 20, 19, 64          # BASELINE config 4's STFT: Hann(20), hop 1, nfft 64
+
+
+@pytest.fixture(scope="module")
+def cfg4():
+    return P.config(4)
+
+
+def _outs(cfg, dev, rd_dtype):
+    import torch
+    M = cfg.max_targets
+    return dict(profile=torch.empty((F, cfg.nr), device=dev),
+                tgt_count=torch.empty(F, dtype=torch.int32, device=dev),
+                tgt_range_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
+                tgt_range_mag=torch.empty((F, M), device=dev),
+                tgt_doppler_idx=torch.empty((F, M), dtype=torch.int32, device=dev),
+                slow_mag=torch.empty((F, cfg.pn), device=dev),
+                rd=torch.empty((F, cfg.nr, cfg.nd, 2), dtype=rd_dtype, device=dev))
+
+
+def _process(eng, cfg, d_iq, dt):
+    import torch
+    o = _outs(cfg, d_iq.device, d_iq.dtype)
+    rd = o.pop("rd")
+    eng.process_device(d_iq, F, dt, o, d_rd=rd, out_dtype=dt, stream=torch.cuda.current_stream())
+    o["rd"] = rd
+    return o
+
+
+def _stft_db(eng, cfg, slow, count):
+    """The bench's STFT leg (stored-P form): compaction of the frames with a target, P and
+    max(P), then 20 log10(P / max) in place; returns the dB rows of the nseg segments."""
+    import torch
+    dev = slow.device
+    s = torch.cuda.current_stream()
+    flist = torch.empty(F, dtype=torch.int32, device=dev)
+    d_len = torch.zeros(1, dtype=torch.int64, device=dev)
+    eng.compact_device(count, F, flist, d_len, stream=s)
+    max_seg = F * cfg.pn + WLEN - 1
+    d_P = torch.empty((max_seg, NFFT // 2 + 1), dtype=torch.float32, device=dev)
+    pmax = torch.zeros(1, dtype=torch.float32, device=dev)
+    nseg = torch.zeros(1, dtype=torch.int64, device=dev)
+    win = torch.tensor(cfg.stft_window(), dtype=torch.float32, device=dev)
+    fs = 1.0 / cfg.prt
+    eng.stft_power_device(slow, flist, d_len, cfg.pn, win, WLEN, NOVERLAP, NFFT, fs, max_seg, d_P, pmax, nseg,
+                          stream=s)
+    eng.stft_db_device(d_P, nseg, max_seg, NFFT, fs, pmax, 0, d_P, stream=s)
+    torch.cuda.synchronize()
+    n = int(nseg.item())
+    assert n > 0.5 * F * cfg.pn                 # most frames hold a target (SURVEY 8d generator)
+    return d_P[:n].clone()
+
+
+def _same(a, b, what):
+    import torch
+    assert a.shape == b.shape, what
+    if not torch.equal(a, b):
+        bad = (a != b).reshape(a.shape[0], -1).any(1).nonzero().flatten()
+        raise AssertionError(f"{what}: {bad.numel()} of {a.shape[0]} rows differ (first {bad[:8].tolist()})")
+
+
+@pytest.mark.parametrize("fp16", [False, True], ids=["c64", "c32h"])
+def test_fullsize_deterministic_and_frame_independent(engine, cfg4, fp16):
+    import torch
+    cfg = cfg4
+    dt = FMCW_C32H if fp16 else FMCW_C64
+    engine.set_taps(cfg, P.synth_calibration(cfg.nts))
+    engine.set_pipeline(FMCW_PIPE_XCD)
+    try:
+        d_iq = torch.empty((F, cfg.pn, cfg.nts, 2), dtype=torch.float16 if fp16 else torch.float32, device="cuda")
+        engine.synth_device(d_iq, 0, F, dt, stream=torch.cuda.current_stream())
+        a = _process(engine, cfg, d_iq, dt)
+        b = _process(engine, cfg, d_iq, dt)
+        engine.synchronize()                      # no hand-off wait timed out
+        for k in a:
+            _same(a[k], b[k], f"run 2 {k}")
+        del b
+        db_a = _stft_db(engine, cfg, a["slow_mag"], a["tgt_count"])
+        db_b = _stft_db(engine, cfg, a["slow_mag"].clone(), a["tgt_count"].clone())
+        _same(db_a, db_b, "STFT dB map")
+        r = _process(engine, cfg, d_iq.flip(0).contiguous(), dt)
+        engine.synchronize()
+        for k in a:
+            _same(r[k].flip(0), a[k], f"reversed {k}")
+        assert int((a["tgt_count"] > 0).sum()) > F // 2
+    finally:
+        engine.set_pipeline(FMCW_PIPE_AUTO)
+        torch.cuda.synchronize()
+
+
+def test_fullsize_power_of_two_scaling(engine, cfg4):
+    import torch
+    cfg = cfg4
+    cal = P.synth_calibration(cfg.nts)
+    engine.set_pipeline(FMCW_PIPE_XCD)
+    try:
+        engine.set_taps(cfg, cal)
+        d_iq = torch.empty((F, cfg.pn, cfg.nts, 2), dtype=torch.float32, device="cuda")
+        engine.synth_device(d_iq, 4096, F, FMCW_C64, stream=torch.cuda.current_stream())
+        a = _process(engine, cfg, d_iq, FMCW_C64)
+        engine.set_taps(cfg, 2 * cal)
+        d_iq.mul_(2)
+        b = _process(engine, cfg, d_iq, FMCW_C64)
+        engine.synchronize()
+        _same(b["rd"], 2 * a["rd"], "RD map x 2")
+        _same(b["profile"], 2 * a["profile"], "profile x 2")
+        # the detection threshold is absolute (:223), so only frames that detect the same bin
+        # are compared row for row; their slow-time rows scale exactly too
+        same = (a["tgt_count"] == b["tgt_count"]) & (a["tgt_range_idx"][:, 0] == b["tgt_range_idx"][:, 0])
+        assert int(same.sum()) > F // 2
+        _same(b["slow_mag"][same], 2 * a["slow_mag"][same], "slow-time rows x 2")
+        # :276-283 the dB map is normalised by max(P): scale-free
+        db1 = _stft_db(engine, cfg, a["slow_mag"], a["tgt_count"])
+        db2 = _stft_db(engine, cfg, 2 * a["slow_mag"], a["tgt_count"])
+        _same(db2, db1, "STFT dB map of the rows x 2")
+    finally:
+        engine.set_taps(cfg, cal)
+        engine.set_pipeline(FMCW_PIPE_AUTO)
+        torch.cuda.synchronize()
