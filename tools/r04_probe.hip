@@ -236,13 +236,13 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
 // read of the slot's previous unit is done), then loads the next unit's input.  2 slots.
 // LAGP: the unit polled and loaded in step j is j - LAGP (1: k_rdx); NS >= 2 LAGP slots (a member
 // that sees ready(j - LAGP) knows every member has read unit j - 2 LAGP)
-template <int UC, int LAGP = 1, int NS = 2>
+template <int UC, int LAGP = 1, int NS = 2, int HB = 1>   // HB 2: every stream at half the bytes (fp16 storage, part K)
 __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
                                                      unsigned* ctr, long nunits, unsigned* err) {
   constexpr int THR = 512;
   static_assert(NS >= 2 * LAGP && NS <= 8, "slot reuse: seeing ready(j - LAGP) proves unit j - 2 LAGP read");
-  constexpr long UB = (long)UC * NR * 8;
-  constexpr int NL = UC * 16 / THR;
+  constexpr long UB = (long)UC * NR * 8 / HB;
+  constexpr int NL = UC * 16 / THR / HB;
   __shared__ int team[2];
   __shared__ unsigned gflag;
   const int tid = threadIdx.x;
@@ -261,8 +261,8 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
   unsigned* ready = ctr + x * 8 * 32;
   char* slots0 = cube + (long)x * NS * UB;
   auto ld_in = [&](long j, f4v (&v)[NL]) __attribute__((always_inline)) {
-    const char* q = iq + (x + 8 * j) * UB + (long)k * (UC / 32) * NR * 8;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(q), (short)0, (UC / 32) * NR * 8, 0x00020000);
+    const char* q = iq + (x + 8 * j) * UB + (long)k * (UC / 32) * NR * 8 / HB;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(q), (short)0, (UC / 32) * NR * 8 / HB, 0x00020000);
 #pragma unroll
     for (int i = 0; i < NL; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 2);
   };
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
     if (pub && tid == 0) __hip_atomic_fetch_add(&ready[((j - 1) % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (dj) {                                     // D(j-1-LAGP): rows from the group loaded in step j-1
       const long f = x + 8L * (j - 1 - LAGP);
-      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)k * 32 * UC * 8, (short)0, 32 * UC * 8, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)k * 32 * UC * 8 / HB, (short)0, 32 * UC * 8 / HB, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NL; ++i) __builtin_amdgcn_raw_buffer_store_b128(grp[i], rr, (tid + THR * i) * 16, 0, 2);
       acc += grp[0];
@@ -288,8 +288,8 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
       } else {
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }
-      const char* g = slots0 + (long)((j - LAGP) % NS) * UB + (long)k * UC * 256;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, UC * 256, 0x00020000);
+      const char* g = slots0 + (long)((j - LAGP) % NS) * UB + (long)k * UC * 256 / HB;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, UC * 256 / HB, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NL; ++i) grp[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 16);
     }
@@ -300,7 +300,7 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(s, (short)0, (int)UB, 0x00020000);
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        const int e = tid + THR * i, ch = k * (UC / 32) + (e >> 9), p = e & 511;
+        const int e = tid + THR * i, ch = k * (UC / 32) + (e / (512 / HB)), p = e % (512 / HB);
         __builtin_amdgcn_raw_buffer_store_b128(xin[i], rs, (((p >> 4) * UC + ch) * 16 + (p & 15)) * 16, 0, 0);
       }
       if (j + 1 < nj) ld_in(j + 1, xin);
@@ -584,6 +584,13 @@ int main(int argc, char** argv) {
     rb("half, done, 3 slots", teamx(k_team_done<128, 3>, 128));
     rb("quarter, done, 2 slots", teamx(k_team_done<64, 2>, 64));
     rb("quarter, done, 4 slots", teamx(k_team_done<64, 4>, 64));
+  }
+  if (part == 11) {
+    printf("== part K: k_rdx's protocol at fp16-storage bytes (input, RD and slots halved; frac on 8.6 GB)\n");
+    auto rh = [&](const char* nm, float ms) { printf("%-44s %.3f ms  frac %.3f (fp16 bytes)\n", nm, ms, algo / 2 / ms / 8.0); };
+    rh("frame, lag 1, 2 slots, fp16 bytes", teamd(k_team_def<256, 1, 2, 2>, 256));
+    rh("frame, lag 2, 4 slots, fp16 bytes", teamd(k_team_def<256, 2, 4, 2>, 256));
+    rb("frame, lag 1, 2 slots, fp32 bytes (part F)", teamd(k_team_def<256, 1, 2>, 256));
   }
   if (part == 7) {
     printf("== part G: the hand-off ring's memory type (CUBE_ALLOC=%d)\n", calloc_flag);
