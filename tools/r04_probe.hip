@@ -390,6 +390,84 @@ __global__ __launch_bounds__(512, 1) void k_team_done(const char* __restrict__ i
   if (acc.x == 1234.5f) rd[tid] = 1;
 }
 
+// Part L: role split.  Members 0-15 of an XCD team only transform (R: 16 chirps of each frame in,
+// their 128 KiB into the slot), members 16-31 only Doppler (D: 2 groups = 128 KiB of the slot in,
+// 128 KiB of RD rows out).  R rewrites slot j % NS once every D member has counted frame j - NS out
+// (done), D reads frame j once every R member has published it (ready): the two roles run decoupled
+// by NS frames of ring.
+template <int NS>
+__global__ __launch_bounds__(512, 1) void k_team_role(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
+                                                      unsigned* ctr, long nunits, unsigned* err) {
+  constexpr int THR = 512, NL = 16;           // 16 x 16 B per thread = 128 KiB per member and frame
+  constexpr long UB = (long)256 * NR * 8;
+  __shared__ int team[2];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7;
+    team[0] = (int)xcc;
+    team[1] = (int)__hip_atomic_fetch_add(ctr + CTR_TICKET + xcc * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
+  if (k >= NK) { atomicOr(err, 2u); return; }
+  const int nj = (int)((nunits - x + 7) / 8);
+  unsigned* ready = ctr + x * 8 * 32;
+  unsigned* done = ctr + CTR_DONE + x * 8 * 32;
+  char* slots0 = cube + (long)x * NS * UB;
+  f4v v[NL], acc{0.f, 0.f, 0.f, 0.f};
+  if (k < 16) {                               // R
+    const int r = k;
+    auto ld_in = [&](long j) __attribute__((always_inline)) {
+      const char* q = iq + (x + 8 * j) * UB + (long)r * 16 * NR * 8;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(q), (short)0, 16 * NR * 8, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 2);
+    };
+    if (nj > 0) ld_in(0);
+    for (int j = 0; j < nj; ++j) {
+      if (j >= NS && tid < 64) wait_ge(&done[(j % NS) * 32], (unsigned)(16 * ((j - NS) / NS + 1)), err + 1);
+      vm_wait<0>();
+      __syncthreads();
+      char* s = slots0 + (long)(j % NS) * UB;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(s, (short)0, (int)UB, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const int e = tid + THR * i, ch = r * 16 + (e >> 9), p = e & 511;   // piece p of chirp ch
+        __builtin_amdgcn_raw_buffer_store_b128(v[i], rs, (((p >> 4) * 256 + ch) * 16 + (p & 15)) * 16, 0, 0);
+      }
+      if (j + 1 < nj) {
+        ld_in(j + 1);
+        vm_wait<NL>();
+      } else {
+        vm_wait<0>();
+      }
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(&ready[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {                                    // D: groups 2d, 2d + 1
+    const int d = k - 16;
+    for (int j = 0; j < nj; ++j) {
+      if (tid < 64) wait_ge(&ready[(j % NS) * 32], (unsigned)(16 * (j / NS + 1)), err + 1);
+      __syncthreads();
+      const char* g = slots0 + (long)(j % NS) * UB + (long)d * 2 * 256 * 256;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(g), (short)0, 2 * 256 * 256, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) v[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + THR * i) * 16, 0, 16);
+      vm_wait<0>();
+      __syncthreads();
+      if (tid == 0) __hip_atomic_fetch_add(&done[(j % NS) * 32], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const long f = x + 8L * j;
+      const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(rd + f * UB + (long)d * 64 * 256 * 8, (short)0, 64 * 256 * 8, 0x00020000);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) __builtin_amdgcn_raw_buffer_store_b128(v[i], rr, (tid + THR * i) * 16, 0, 2);
+      acc += v[0];
+    }
+  }
+  if (acc.x == 1234.5f) rd[tid] = 1;
+}
+
 // ---------------------------------------------------------------- part C: stores leaving the L2
 // every CU rewrites its own R-byte region `passes` times with policy AUX (16-byte stores);
 // WRITE_SIZE / bytes stored says whether each pass leaves the XCD's L2
@@ -584,6 +662,13 @@ int main(int argc, char** argv) {
     rb("half, done, 3 slots", teamx(k_team_done<128, 3>, 128));
     rb("quarter, done, 2 slots", teamx(k_team_done<64, 2>, 64));
     rb("quarter, done, 4 slots", teamx(k_team_done<64, 4>, 64));
+  }
+  if (part == 12) {
+    printf("== part L: role split (16 range members, 16 Doppler members per XCD; NS frames of ring)\n");
+    rb("frame, lag 1, 2 slots (part F)", teamd(k_team_def<256, 1, 2>, 256));
+    rb("roles, 2 slots", teamx(k_team_role<2>, 256));
+    rb("roles, 3 slots", teamx(k_team_role<3>, 256));
+    rb("roles, 4 slots", teamx(k_team_role<4>, 256));
   }
   if (part == 11) {
     printf("== part K: k_rdx's protocol at fp16-storage bytes (input, RD and slots halved; frac on 8.6 GB)\n");
