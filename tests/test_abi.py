@@ -114,3 +114,16 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.FmcwError, match="not found"):
         _lib.load()
+
+
+def test_stream_handles_of_device_calls():
+    """engine._sided: None -> NULL (the context's own stream), a raw handle and a torch stream with
+    a non-zero handle pass through unchanged; only torch's default stream (handle 0) is routed
+    through a joined side stream (GPU-side: tests/test_gpu_fullsize.py)."""
+    from fmcw_radar_processing_amd.engine import _sided
+
+    class _S:                       # a torch.cuda.Stream stand-in with a non-default handle
+        cuda_stream = 0x1234
+    for arg, want in ((None, None), (7, 7), (_S(), 0x1234)):
+        with _sided(arg) as h:
+            assert h.value == want
