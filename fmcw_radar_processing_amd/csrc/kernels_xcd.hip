@@ -73,10 +73,16 @@ using namespace op;
 #define XK_RD_AUX 2                    // RD store cache policy: nt (A/B: 16 = sc1, 17 = sc0 sc1, 18 = sc1 nt, 3 = sc0 nt)
 #endif
 constexpr int kRdAux = XK_RD_AUX;
-#ifndef XK_NS
-#define XK_NS 2
+#ifndef XK_LAG
+#define XK_LAG 1                       // A/B: the group polled and loaded in step j is frame j - XK_LAG
 #endif
+#ifndef XK_NS
+#define XK_NS (2 * XK_LAG)
+#endif
+constexpr int kLag = XK_LAG;
+static_assert(kLag == 1 || kLag == 2, "poll lag 1 (shipped) or 2");
 constexpr int kNS = XK_NS;            // hand-off slots in use per XCD (2..XCD_MAX_SLOTS; see the step loop)
+static_assert(kNS >= 2 * kLag && kNS <= 4, "slot reuse: seeing ready(j - lag) proves frame j - 2 lag read");
 constexpr int NK = 32;                 // team members (CUs) per XCD
 constexpr int C = 256;                 // chirps = Doppler points
 constexpr int NW = 8;                  // waves per workgroup = chirps per member
@@ -602,7 +608,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // flags: std::integral_constant (folded: straight-line copies) or bool (the short-launch copy)
   auto body = [&](int j, auto DJ, auto RJ, auto PUB, auto CNT, auto GJ, auto NEXT, auto G16) __attribute__((always_inline)) {
     const bool dj = DJ, rj = RJ, pub = PUB, gj = GJ, next = NEXT;
-    const int64_t fd = frame(j - 2);
+    const int64_t fd = frame(j - 1 - kLag);
     if (j >= 1) __syncthreads();       // B1: step j - 1 done in every wave (transpose regions, keys, x0)
     stamp(0);
 #ifndef XK_NOREF
@@ -648,12 +654,12 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     if (gj) {   // wave 0 polls ready(j - 1) (scalar: its vector memory operations stay in flight) and
                 // tells the other waves through LDS; then every wave loads its share of group k
       if (w == 0) {
-        wait_ge(&ready[((j - 1) % kNS) * 32], (unsigned)(NK * ((j - 1) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);
+        wait_ge(&ready[((j - kLag) % kNS) * 32], (unsigned)(NK * ((j - kLag) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);
         if (lane == 0) *reinterpret_cast<volatile unsigned*>(&gflag) = (unsigned)j;
       } else {
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }
-      ld_group(slot(j - 1) + (int64_t)k * C * GP * kES, grp, G16);
+      ld_group(slot(j - kLag) + (int64_t)k * C * GP * kES, grp, G16);
     }
     stamp(7);
     if (dj) d_td(xv);
@@ -674,6 +680,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       r_mid(u);
       r_t2(u, q0, q1);
 #ifdef XK_DONE
+      static_assert(kLag == 1, "the done-counter A/B is written for lag 1");
       // one slot: every member's group loads of frame j - 1 (issued above) must have returned
       // before R(j) rewrites it.  Count them out (done), then wait for the whole team.
       if (gj) {
@@ -699,6 +706,24 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   using C1 = std::integral_constant<int, 0>;
   using CF = std::integral_constant<int, kRDs>;
   auto run = [&](auto G16) __attribute__((always_inline)) {
+#if XK_LAG == 2
+    // lag 2: the Doppler runs three steps behind; 4 slots
+    if (nj >= 5) {
+      //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
+      body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{}, G16);
+      body(1,      F_{}, T_{}, T_{}, C0{},                          F_{}, T_{}, G16);
+      body(2,      F_{}, T_{}, T_{}, C0{},                          T_{}, T_{}, G16);
+      body(3,      T_{}, T_{}, T_{}, C0{},                          T_{}, T_{}, G16);
+      for (int j = 4; j < nj; ++j) body(j, T_{}, T_{}, T_{}, CF{}, T_{}, T_{}, G16);
+      body(nj,     T_{}, F_{}, T_{}, CF{},                          T_{}, F_{}, G16);
+      body(nj + 1, T_{}, F_{}, F_{}, C0{},                          T_{}, F_{}, G16);
+      body(nj + 2, T_{}, F_{}, F_{}, C0{},                          F_{}, F_{}, G16);
+    } else {
+      for (int j = 0; j < nj + 3; ++j)
+        body(j, j >= 3, j < nj, j >= 1 && j - 1 < nj, C0{}, j >= 2 && j - 2 < nj, j + 1 < nj, G16);
+    }
+    return;
+#endif
     if (nj >= 3) {
       //   j       DJ   RJ   PUB  CNT                              GJ   NEXT
       body(0,      F_{}, T_{}, F_{}, C0{},                          F_{}, T_{}, G16);
