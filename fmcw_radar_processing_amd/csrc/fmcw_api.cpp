@@ -71,6 +71,16 @@ struct DevBuf {
   ~DevBuf() { release(); }
 };
 
+// Offsets of several arrays packed into one buffer (256-byte aligned).
+struct Arena {
+  size_t off = 0;
+  size_t add(size_t bytes) {
+    const size_t o = off;
+    off += (bytes + 255) & ~(size_t)255;
+    return o;
+  }
+};
+
 // Page-locked host staging buffer (DMA source / target of the host-pointer calls).
 struct PinBuf {
   void* p = nullptr;
@@ -194,11 +204,15 @@ struct fmcw_ctx {
   // each, so chunk i+1's H2D copy (stream cin) and chunk i-1's D2H copy (cout)
   // run under chunk i's kernels (the caller's data is copied into the pinned
   // slots by host threads meanwhile)
-  DevBuf h_iq, h_prof, h_count, h_ridx, h_rmag, h_didx, h_slow, h_rd, h_probe;
+  DevBuf h_iq, h_prof, h_rd;
   PinBuf pin_in, pin_out;
+  // small per-call arrays of the host-pointer calls, packed so that they cross PCIe as ONE copy
+  // (each pageable copy costs ~20-30 us of latency: six of them were half of a deployed call)
+  DevBuf h_small, s_in;
+  PinBuf pin_small, pin_sin;
   hipStream_t cin = nullptr, cout = nullptr;
   hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
-  DevBuf s_x, s_list, s_len, s_P, s_pmax, s_nseg, s_win, s_lidx, s_lw, s_out, s_bins;
+  DevBuf s_P, s_pmax, s_nseg, s_lidx, s_lw, s_out;
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
   // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one: device calls on
   // different streams (with different windows or nfft) never share a table.  At most kTabs of
@@ -1300,6 +1314,10 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     for (auto& i0 : lidx) i0 = pos[i0];   // i0 and i0+1 are both listed, so they are adjacent columns
   }
   const int ncolP = sel_mode ? (int)bins.size() : nb;
+  // per device, the call's inputs (its samples, the one-entry frame list, the length, the window,
+  // the listed bins and the interp1 table) in one arena: one pinned H2D copy instead of seven
+  struct InOff { size_t x, list, len, win, bins, lidx, lw; };
+  std::vector<InOff> io(world);
   // Segments are sharded contiguously over the devices; device g takes the
   // samples its segments cover (its halo is simply the next samples of x).
   // 1) P and the local max(P) per device
@@ -1310,32 +1328,43 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     CHK(set_device(d));
     hipStream_t s = d->stream;
     const int64_t Ld = ns > 0 ? (ns - 1) * hop + wlen : 0;
-    CHK(d->s_x.ensure((size_t)std::max<int64_t>(Ld, 1) * 4));
-    CHK(d->s_list.ensure(4));
-    CHK(d->s_len.ensure(8));
     CHK(d->s_P.ensure((size_t)std::max<int64_t>(ns, 1) * ncolP * 4));
     CHK(d->s_pmax.ensure(4));
     CHK(d->s_nseg.ensure(8));
-    CHK(d->s_win.ensure((size_t)wlen * 4));
     CHK(d->s_out.ensure((size_t)std::max<int64_t>(ns, 1) * nbo * 4));
     HIPCHK(hipMemsetAsync(d->s_pmax.p, 0, 4, s));
     if (ns == 0) continue;
-    const int32_t zero = 0;
-    HIPCHK(hipMemcpyAsync(d->s_x.p, x + s0 * hop, (size_t)Ld * 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d->s_list.p, &zero, 4, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d->s_len.p, &Ld, 8, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d->s_win.p, win, (size_t)wlen * 4, hipMemcpyHostToDevice, s));
+    Arena ar;
+    InOff& o = io[g];
+    o.x = ar.add((size_t)Ld * 4); o.list = ar.add(4); o.len = ar.add(8); o.win = ar.add((size_t)wlen * 4);
+    o.bins = ar.add(bins.size() * 4); o.lidx = ar.add(lidx.size() * 4); o.lw = ar.add(lw.size() * 4);
+    CHK(d->s_in.ensure(ar.off));
+    CHK(d->pin_sin.ensure(ar.off));
+    {
+      char* h = d->pin_sin.at(0);
+      par_memcpy(h + o.x, x + s0 * hop, (size_t)Ld * 4);
+      const int32_t zero = 0;
+      std::memcpy(h + o.list, &zero, 4);
+      std::memcpy(h + o.len, &Ld, 8);
+      std::memcpy(h + o.win, win, (size_t)wlen * 4);
+      if (!bins.empty()) std::memcpy(h + o.bins, bins.data(), bins.size() * 4);
+      if (!lidx.empty()) std::memcpy(h + o.lidx, lidx.data(), lidx.size() * 4);
+      if (!lw.empty()) std::memcpy(h + o.lw, lw.data(), lw.size() * 4);
+    }
+    HIPCHK(hipMemcpyAsync(d->s_in.p, d->pin_sin.p, ar.off, hipMemcpyHostToDevice, s));
+    char* const di = d->s_in.as<char>();
+    float* const d_x = reinterpret_cast<float*>(di + o.x);
+    int32_t* const d_list = reinterpret_cast<int32_t*>(di + o.list);
+    int64_t* const d_len = reinterpret_cast<int64_t*>(di + o.len);
+    float* const d_win = reinterpret_cast<float*>(di + o.win);
     // the shard's samples are one "frame" of Ld samples in the compaction indirection
-    CHK(fmcw_stft_power_device(d, d->s_x.as<float>(), d->s_list.as<int32_t>(), d->s_len.as<int64_t>(), (int32_t)Ld,
-                               nullptr, 0, nullptr, d->s_win.as<float>(), wlen, noverlap, nf, fs, ns,
+    CHK(fmcw_stft_power_device(d, d_x, d_list, d_len, (int32_t)Ld, nullptr, 0, nullptr, d_win, wlen, noverlap, nf, fs, ns,
                                sel_mode ? nullptr : d->s_P.as<float>(), d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
     if (sel_mode) {   // second pass: P of the listed bins (the W table of the first pass is reused)
-      CHK(d->s_bins.ensure(bins.size() * 4));
-      HIPCHK(hipMemcpyAsync(d->s_bins.p, bins.data(), bins.size() * 4, hipMemcpyHostToDevice, s));
       fmcw::StftArgs a{};
-      a.slow_mag = d->s_x.as<float>(); a.frame_list = d->s_list.as<int32_t>(); a.len = d->s_len.as<int64_t>();
-      a.pn = (int32_t)Ld; a.win = d->s_win.as<float>(); a.wlen = wlen; a.hop = hop; a.nfft = nf;
-      a.inv_fs = (float)(1.0 / fs); a.max_seg = ns; a.bins = d->s_bins.as<int32_t>(); a.ncol = ncolP;
+      a.slow_mag = d_x; a.frame_list = d_list; a.len = d_len;
+      a.pn = (int32_t)Ld; a.win = d_win; a.wlen = wlen; a.hop = hop; a.nfft = nf;
+      a.inv_fs = (float)(1.0 / fs); a.max_seg = ns; a.bins = reinterpret_cast<int32_t*>(di + o.bins); a.ncol = ncolP;
       StageTimer tm(d, 4, s);
       int st = FMCW_OK;
       float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table on s
@@ -1344,7 +1373,7 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       CHK(d->stft_tab_done(s));
       tm.done();
     }
-    HIPCHK(hipStreamSynchronize(s));   // the host-side scalars above go out of scope
+    HIPCHK(hipStreamSynchronize(s));   // local max(P) final (step 2 may read it through the host)
   }
   // 2) the global max(P) of :282-283: RCCL all_reduce(max) across the devices
   if (world > 1) {
@@ -1412,15 +1441,12 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     if (ns == 0) continue;
     CHK(set_device(d));
     hipStream_t s = d->stream;
-    if (sel_mode) {   // interp1 over the listed columns (lidx holds column positions)
-      CHK(d->s_lidx.ensure(lidx.size() * 4));
-      CHK(d->s_lw.ensure(lw.size() * 4));
-      HIPCHK(hipMemcpyAsync(d->s_lidx.p, lidx.data(), lidx.size() * 4, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(d->s_lw.p, lw.data(), lw.size() * 4, hipMemcpyHostToDevice, s));
+    if (sel_mode) {   // interp1 over the listed columns (lidx holds column positions; uploaded in step 1)
       fmcw::StftDbArgs a{};
       a.P = d->s_P.as<float>(); a.nseg = d->s_nseg.as<int64_t>(); a.max_seg = ns; a.nbins_in = ncolP;
       a.pmax = d->s_pmax.as<float>(); a.nlog = n_log_bins;
-      a.lidx = d->s_lidx.as<int32_t>(); a.lw = d->s_lw.as<float>(); a.out = d->s_out.as<float>();
+      a.lidx = reinterpret_cast<int32_t*>(d->s_in.as<char>() + io[g].lidx);
+      a.lw = reinterpret_cast<float*>(d->s_in.as<char>() + io[g].lw); a.out = d->s_out.as<float>();
       StageTimer tm(d, 5, s);
       HIPCHK(fmcw::launch_stft_db(a, s));
       tm.done();
@@ -1550,32 +1576,35 @@ static int process_host_one(fmcw_ctx* c, const fmcw_params* p, const void* iq, i
   if (in_dtype != FMCW_C64 && in_dtype != FMCW_C32H) return fail(FMCW_E_ARG, "bad in_dtype");
   const int S = p->nts, C = p->pn, NR = p->nr, ND = p->nd, M = p->max_targets;
   hipStream_t s = c->stream;
-  CHK(c->h_prof.ensure((size_t)F * NR * 4));
-  CHK(c->h_count.ensure((size_t)F * 4));
-  CHK(c->h_ridx.ensure((size_t)F * M * 4));
-  CHK(c->h_rmag.ensure((size_t)F * M * 4));
-  CHK(c->h_didx.ensure((size_t)F * M * 4));
-  CHK(c->h_slow.ensure((size_t)F * C * 4));
-  if (probe) CHK(c->h_probe.ensure((size_t)NR * 4));
+  // the small outputs in one device arena, back through one pinned copy
+  Arena ar;
+  const size_t o_prof = ar.add((size_t)F * NR * 4), o_count = ar.add((size_t)F * 4), o_ridx = ar.add((size_t)F * M * 4),
+               o_rmag = ar.add((size_t)F * M * 4), o_didx = ar.add((size_t)F * M * 4), o_slow = ar.add((size_t)F * C * 4),
+               o_probe = ar.add(probe ? (size_t)NR * 4 : 0);
+  CHK(c->h_small.ensure(ar.off));
+  CHK(c->pin_small.ensure(ar.off));
+  char* const hs = c->h_small.as<char>();
+  auto at = [&](size_t o) { return reinterpret_cast<float*>(hs + o); };
+  auto ati = [&](size_t o) { return reinterpret_cast<int32_t*>(hs + o); };
   const size_t fin = (size_t)C * S * esize(in_dtype);
   const BigOut big[2] = {{reinterpret_cast<char*>(cube), (size_t)C * NR * 8}, {reinterpret_cast<char*>(rd), (size_t)NR * ND * 8}};
   CHK(host_pipeline(c, iq, F, fin, big, [&](char* d_in, int64_t f0, int64_t nf, char* const* d_big) {
     const int64_t pc = probe && probe_column > f0 * C && probe_column <= (f0 + nf) * C ? probe_column - f0 * C : 0;
-    return fmcw_process_device(c, p, d_in, in_dtype, nf, c->h_prof.as<float>() + f0 * NR, c->h_count.as<int32_t>() + f0,
-                               c->h_ridx.as<int32_t>() + f0 * M, c->h_rmag.as<float>() + f0 * M,
-                               c->h_didx.as<int32_t>() + f0 * M, c->h_slow.as<float>() + f0 * C,
-                               d_big[0], d_big[1], FMCW_C64, pc,
-                               pc ? c->h_probe.as<float>() : nullptr, s);
+    return fmcw_process_device(c, p, d_in, in_dtype, nf, at(o_prof) + f0 * NR, ati(o_count) + f0, ati(o_ridx) + f0 * M,
+                               at(o_rmag) + f0 * M, ati(o_didx) + f0 * M, at(o_slow) + f0 * C, d_big[0], d_big[1], FMCW_C64,
+                               pc, pc ? at(o_probe) : nullptr, s);
   }));
-  HIPCHK(hipMemcpyAsync(prof, c->h_prof.p, (size_t)F * NR * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(count, c->h_count.p, (size_t)F * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(ridx, c->h_ridx.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(rmag, c->h_rmag.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(didx, c->h_didx.p, (size_t)F * M * 4, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(slow, c->h_slow.p, (size_t)F * C * 4, hipMemcpyDeviceToHost, s));
-  if (probe) HIPCHK(hipMemcpyAsync(probe, c->h_probe.p, (size_t)NR * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(c->pin_small.p, hs, ar.off, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   HIPCHK(hipStreamSynchronize(c->cout));
+  const char* ps = c->pin_small.at(0);
+  par_memcpy(prof, ps + o_prof, (size_t)F * NR * 4);
+  std::memcpy(count, ps + o_count, (size_t)F * 4);
+  std::memcpy(ridx, ps + o_ridx, (size_t)F * M * 4);
+  std::memcpy(rmag, ps + o_rmag, (size_t)F * M * 4);
+  std::memcpy(didx, ps + o_didx, (size_t)F * M * 4);
+  par_memcpy(slow, ps + o_slow, (size_t)F * C * 4);
+  if (probe) std::memcpy(probe, ps + o_probe, (size_t)NR * 4);
   return xcd_check(c);
 }
 
