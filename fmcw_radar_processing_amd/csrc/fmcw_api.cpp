@@ -922,17 +922,23 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
   const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
   hipStream_t sd = c->sd, sx = c->sx;
+  // one chunk: K1 -> K2 -> K3 have nothing to overlap with, so they go on the caller's stream
+  // without the fork / join events (a deployed 115-frame call: 9 event calls fewer)
+  if (F <= chunk) sd = sx = s;
   if (const char* e = std::getenv("FMCW_ONE_STREAM"); e && e[0] == '1') sd = sx = s;   // A/B probe
+  const bool split = sd != s || sx != s;
   StageTimer span(c, 7, s, 1);     // range+Doppler span: before K1(0) on s ... after the last K2 on sd
-  HIPCHK(hipEventRecord(c->ev_fork, s));
-  HIPCHK(hipStreamWaitEvent(sd, c->ev_fork, 0));
-  HIPCHK(hipStreamWaitEvent(sx, c->ev_fork, 0));
+  if (split) {
+    HIPCHK(hipEventRecord(c->ev_fork, s));
+    HIPCHK(hipStreamWaitEvent(sd, c->ev_fork, 0));
+    HIPCHK(hipStreamWaitEvent(sx, c->ev_fork, 0));
+  }
 
   int64_t i = 0;
   for (int64_t f0 = 0; f0 < F; f0 += chunk, ++i) {
     const int b = (int)(i % NS);
     const int64_t nf = std::min(chunk, F - f0);
-    if (i >= NS) HIPCHK(hipStreamWaitEvent(s, c->ev_k3[b], 0));   // WAR: K2/K3(i-NS) done with slot b
+    if (split && i >= NS) HIPCHK(hipStreamWaitEvent(s, c->ev_k3[b], 0));   // WAR: K2/K3(i-NS) done with slot b
     char* cube = d_cube ? static_cast<char*>(d_cube) + (size_t)f0 * C * NR * esize(cube_dt)
                         : c->scratch_cube.as<char>() + b * cube_slot;
     char* rd = d_rd ? static_cast<char*>(d_rd) + (size_t)f0 * NR * ND * esize(rd_dt)
@@ -957,8 +963,10 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
       HIPCHK(fmcw::launch_range(ra, s));
       tm.done();
     }
-    HIPCHK(hipEventRecord(c->ev_k1[b], s));
-    HIPCHK(hipStreamWaitEvent(sd, c->ev_k1[b], 0));
+    if (split) {
+      HIPCHK(hipEventRecord(c->ev_k1[b], s));
+      HIPCHK(hipStreamWaitEvent(sd, c->ev_k1[b], 0));
+    }
 
     fmcw::DopplerArgs da{};
     da.cube = cube; da.cube_dtype = cube_dt;
@@ -973,8 +981,10 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
       HIPCHK(fmcw::launch_doppler(da, sd));
       tm.done();
     }
-    HIPCHK(hipEventRecord(c->ev_k2[b], sd));
-    HIPCHK(hipStreamWaitEvent(sx, c->ev_k2[b], 0));
+    if (split) {
+      HIPCHK(hipEventRecord(c->ev_k2[b], sd));
+      HIPCHK(hipStreamWaitEvent(sx, c->ev_k2[b], 0));
+    }
 
     fmcw::DetectArgs ka{};
     ka.profile = d_prof + f0 * NR;
@@ -998,13 +1008,15 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
       HIPCHK(fmcw::launch_detect(ka, sx));
       tm.done();
     }
-    HIPCHK(hipEventRecord(c->ev_k3[b], sx));
+    if (split) HIPCHK(hipEventRecord(c->ev_k3[b], sx));
   }
   span.s = sd;
   span.done();
   // join: the caller's stream waits for the last detect (which follows every K2)
-  HIPCHK(hipEventRecord(c->ev_join, sx));
-  HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+  if (split) {
+    HIPCHK(hipEventRecord(c->ev_join, sx));
+    HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
+  }
   return FMCW_OK;
 }
 
@@ -1373,7 +1385,7 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       CHK(d->stft_tab_done(s));
       tm.done();
     }
-    HIPCHK(hipStreamSynchronize(s));   // local max(P) final (step 2 may read it through the host)
+    if (world > 1) HIPCHK(hipStreamSynchronize(s));   // local max(P) final (step 2 may read it through the host)
   }
   // 2) the global max(P) of :282-283: RCCL all_reduce(max) across the devices
   if (world > 1) {
@@ -1530,8 +1542,13 @@ static int host_pipeline(fmcw_ctx* c, const void* iq, int64_t F, size_t fin, con
                    (size_t)nf * big[q].fbytes);
     return FMCW_OK;
   };
-  HIPCHK(hipEventRecord(c->ev_fork, s));          // the device buffers are free once earlier work on s is done
-  HIPCHK(hipStreamWaitEvent(c->cin, c->ev_fork, 0));
+  // one chunk: its H2D copy has nothing to overlap with and goes on s (no fork / join events)
+  const bool single = n == 1;
+  hipStream_t cin = single ? s : c->cin;
+  if (!single) {
+    HIPCHK(hipEventRecord(c->ev_fork, s));          // the device buffers are free once earlier work on s is done
+    HIPCHK(hipStreamWaitEvent(c->cin, c->ev_fork, 0));
+  }
   for (int64_t i = 0; i < n; ++i) {
     const int b = (int)(i & 1);
     const int64_t f0 = i * Fc, nf = std::min(Fc, F - f0);
@@ -1539,9 +1556,11 @@ static int host_pipeline(fmcw_ctx* c, const void* iq, int64_t F, size_t fin, con
     par_memcpy(c->pin_in.at(b * slot_in), static_cast<const char*>(iq) + (size_t)f0 * fin, (size_t)nf * fin);
     if (i >= 2) HIPCHK(hipStreamWaitEvent(c->cin, c->ev_comp[b], 0));   // device slot b: chunk i-2's kernels are done
     HIPCHK(hipMemcpyAsync(c->h_iq.as<char>() + b * slot_in, c->pin_in.at(b * slot_in), (size_t)nf * fin,
-                          hipMemcpyHostToDevice, c->cin));
-    HIPCHK(hipEventRecord(c->ev_h2d[b], c->cin));
-    HIPCHK(hipStreamWaitEvent(s, c->ev_h2d[b], 0));
+                          hipMemcpyHostToDevice, cin));
+    if (!single) {
+      HIPCHK(hipEventRecord(c->ev_h2d[b], c->cin));
+      HIPCHK(hipStreamWaitEvent(s, c->ev_h2d[b], 0));
+    }
     if (any && i >= 2) {                          // device out slot b: chunk i-2's D2H has read it
       HIPCHK(hipStreamWaitEvent(s, c->ev_d2h[b], 0));
       CHK(drain(i - 2));                          // and its rows go to the caller (pinned slot b is reused below)
