@@ -15,10 +15,11 @@ from fmcw_radar_processing_amd import windows as W  # noqa: E402
 from fmcw_radar_processing_amd.engine import Engine  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+geom = sys.argv[2] if len(sys.argv) > 2 else "deployed"     # or "3": 256 config-3 frames (bench host_path)
 eng = Engine(0)
-cfg = P.config("deployed")
+cfg = P.config("deployed" if geom == "deployed" else int(geom))
 eng.set_taps(cfg, P.synth_calibration(cfg.nts))
-F = 115
+F = 115 if geom == "deployed" else 256
 d = torch.empty((F, cfg.pn, cfg.nts, 2), dtype=torch.float32, device="cuda")
 eng.synth_device(d, 0, F, FMCW_C64)
 torch.cuda.synchronize()
