@@ -267,7 +267,12 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     else { const int t = (i - XT_D1) >> 6; d = reinterpret_cast<c2*>(&L.twd[t >> 1][l]) + (t & 1); }
     *d = v;
   }
-  for (int i = tid; i < 16 * 64; i += 512) reinterpret_cast<float*>(&L.wdl[i >> 8][i & 63])[(i >> 6) & 3] = a.wd[(i & 15) + 16 * (i >> 6)];
+  // the Doppler window carries the two power-of-two scales of fp16 storage (exact, so the outputs
+  // keep their bits): the RD map's 1 / (Nr Nd) and, for a member whose group is handed over as
+  // c32h, the Nr its staging no longer multiplies back in (VALU work taken out of every step)
+  const float wd_scale = (H && RD ? a.rd_scale : 1.0f) * (g16 ? kXU : 1.0f);
+  for (int i = tid; i < 16 * 64; i += 512)
+    reinterpret_cast<float*>(&L.wdl[i >> 8][i & 63])[(i >> 6) & 3] = a.wd[(i & 15) + 16 * (i >> 6)] * wd_scale;
   // :203-205 per-lane constants of samples n = 2 lane + e + 128 i: w' = IF_scale 2blackman, cal w'
   for (int i = tid; i < 16 * 64; i += 512) {
     const int l = i & 63, v = i >> 6, n = 2 * l + (v & 1) + 128 * (v >> 1);
@@ -441,7 +446,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
         const u4v u = __builtin_bit_cast(u4v, t[i]);
         const float2 a0 = h2f(u.x), a1 = h2f(u.y), a2 = h2f(u.z), a3 = h2f(u.w);
         f4v* d = &L.u.stg[(e >> 3) * 17 + (e & 7) * 2];
-        const f4v lo = f4v{a0.x, a0.y, a1.x, a1.y} * kXU, hi = f4v{a2.x, a2.y, a3.x, a3.y} * kXU;
+        // kept as X / Nr: the rows below scale their outputs, the Doppler window the rest
+        const f4v lo = f4v{a0.x, a0.y, a1.x, a1.y}, hi = f4v{a2.x, a2.y, a3.x, a3.y};
         // lanes 4-7 of each 8-lane store group write their upper half first: the group's 8 stores
         // then hit 8 different 16-byte bank groups (conflict-free ds_write_b128)
         const bool sw = (e >> 2) & 1;
@@ -459,7 +465,8 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const int pp = lane >> 4, q = lane & 15, p = 4 * w + pp;
   const int r = xcd_bin(k, p);
   // D1: the rows from the staged group, :217 row mean, :210 / :265 row max |X| -> profile, candidate keys
-  auto d_rows = [&](int64_t f, c2 (&xv)[16], c2& x0r, c2& mu) __attribute__((always_inline)) {
+  // G16: the staged group holds X / Nr (c32h hand-off): the profile and the keys are scaled back here
+  auto d_rows = [&](int64_t f, c2 (&xv)[16], c2& x0r, c2& mu, auto G16) __attribute__((always_inline)) {
     {
       const c2* stg = reinterpret_cast<const c2*>(L.u.stg);
 #pragma unroll
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     sm = c2{row_sum16(sm.x), row_sum16(sm.y)};
     pm = __int_as_float(row_max16(__float_as_int(pm)));
     mu = sm * (1.0f / (float)C);
-    const float pr = sqrtf(pm);
+    const float pr = decltype(G16)::value ? sqrtf(pm) * kXU : sqrtf(pm);
     a.profile[f * NR + r] = pr;        // all 16 lanes of the row (same value): a store on every path
     if (q == 0) {
       const double rng = (double)r * a.dist_per_bin;
@@ -501,7 +508,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   };
   // D2 (after the keys barrier): slow-time candidates (:257-259), the XCD_CAND strongest
   // in-window rows of the group
-  auto d_cand = [&](int64_t f, const c2 (&xv)[16], c2 x0r) __attribute__((always_inline)) {
+  auto d_cand = [&](int64_t f, const c2 (&xv)[16], c2 x0r, auto G16) __attribute__((always_inline)) {
     float kv = lane < GP ? L.key[lane] : -1.f;
     const int ki = xcd_bin(k, lane & (GP - 1));
 #pragma unroll
@@ -514,7 +521,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       if (sel >= 0 && r == sel) {
         float* __restrict__ row = a.cand_rows + ((f * XCD_TILES + k) * XCD_CAND + c) * (int64_t)C;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) row[q + 16 * i] = abs2v(xv[i] + x0r);
+        for (int i = 0; i < 16; ++i) {
+          const float v = abs2v(xv[i] + x0r);
+          row[q + 16 * i] = decltype(G16)::value ? v * (kXU * kXU) : v;
+        }
       }
       if (ki == sel) kv = -1.f;
     }
@@ -558,7 +568,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       for (int d1s = 0; d1s < 16; ++d1s) {
         const int off = r * C + q + 16 * d1s;
         if constexpr (H) {
-          const c2 o = xv[(d1s + 8) & 15] * a.rd_scale;
+          const c2 o = xv[(d1s + 8) & 15];                 // rd_scale is in the window
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, __floats2half2_rn(o.x, o.y)), rr, off * 4, 0,
                                                 kRdAux);
         } else {
@@ -635,11 +645,11 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     stamp(2);
     c2 z0[8], z1[8], u[16];
     c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
-    if (dj) d_rows(fd, xv, x0r, dmu);
+    if (dj) d_rows(fd, xv, x0r, dmu, G16);
     stamp(3);
     if (dj) __syncthreads();           // B3: keys in, staging read out
     stamp(4);
-    if (dj) d_cand(fd, xv, x0r);
+    if (dj) d_cand(fd, xv, x0r, G16);
     stamp(5);
     if (rj) r_prep(xin, z0, z1);
     if (next) {                        // R1 freed the chirp registers: the next frame's loads go out
