@@ -213,6 +213,7 @@ struct fmcw_ctx {
   hipStream_t cin = nullptr, cout = nullptr;
   hipEvent_t ev_h2d[2] = {}, ev_comp[2] = {}, ev_d2h[2] = {};
   DevBuf s_P, s_pmax, s_nseg, s_lidx, s_lw, s_out;
+  DevBuf s_cbins, s_segmax, s_tiles;   // fmcw_stft's coarse-to-fine max(P) (stft_coarse_max)
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
   // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one: device calls on
   // different streams (with different windows or nfft) never share a table.  At most kTabs of
@@ -271,6 +272,7 @@ struct fmcw_ctx {
     return FMCW_OK;
   }
   int64_t chunk_frames = 0;
+  int64_t last_coarse_tiles = -1;     // tiles the last coarse-to-fine max(P) evaluated in full (diagnostics)
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
   DevBuf k1_part;                               // K1's per-workgroup profile maxima (range-only calls)
@@ -1293,6 +1295,58 @@ static int d2h_big(fmcw_ctx* c, void* dst, const void* d_src, size_t bytes, hipS
   return FMCW_OK;
 }
 
+// max(P) of :282-283 over every bin of a large nfft without evaluating every bin of every segment.
+// |X_s(w)| of a 20-tap segment is a trigonometric polynomial of degree 19, so (Bernstein) within one
+// coarse step h = 2 pi / K of its peak it is at least (1 - 19 h) of the peak.  Pass 1 takes each
+// segment's max over the coarse bins k = m nfft / K (exact P values of the fine grid, so their
+// maximum G is a lower bound of max(P)); a segment whose coarse max is below G (1 - 19 h)^2 cannot
+// hold max(P).  Pass 2 takes the max over every bin of the 256-segment tiles that hold a
+// candidate: the same P values the full pass would compare, so the result is the same bits.
+static int stft_coarse_max(fmcw_ctx* d, const fmcw::StftArgs& a0, hipStream_t s) {
+  constexpr int K = 16384;
+  const int nf = a0.nfft, D = nf / K, nc = K / 2 + 1;
+  const int64_t ns = a0.max_seg;
+  std::vector<int32_t> cb(nc);
+  for (int m = 0; m < nc; ++m) cb[m] = D * m;
+  CHK(d->s_cbins.ensure((size_t)nc * 4));
+  CHK(d->s_segmax.ensure((size_t)ns * 4));
+  int st = FMCW_OK;
+  float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);
+  CHK(st);
+  HIPCHK(hipMemcpyAsync(d->s_cbins.p, cb.data(), (size_t)nc * 4, hipMemcpyHostToDevice, s));
+  HIPCHK(fmcw::launch_stft_table(a0.win, nf, tab, s));
+  fmcw::StftArgs a = a0;
+  a.bins = d->s_cbins.as<int32_t>();
+  a.ncol = nc;
+  HIPCHK(fmcw::launch_stft20(a, tab, 4, d->s_segmax.as<float>(), s));
+  std::vector<float> sm((size_t)ns);
+  HIPCHK(hipMemcpyAsync(sm.data(), d->s_segmax.p, (size_t)ns * 4, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  float G = 0.f;
+  for (float v : sm) G = std::max(G, v);
+  const double f = 1.0 - (double)(a0.wlen - 1) * 2.0 * M_PI / K;   // degree wlen - 1 (the 20-tap fast path)
+  const float thr = (float)((double)G * f * f * (1.0 - 1e-3));   // margin for the fp32 rounding of P
+  std::vector<int32_t> tiles;
+  for (int64_t t = 0; t * 256 < ns; ++t) {
+    const int64_t e = std::min<int64_t>(ns, (t + 1) * 256);
+    for (int64_t i = t * 256; i < e; ++i)
+      if (sm[(size_t)i] >= thr) { tiles.push_back((int32_t)t); break; }
+  }
+  CHK(d->s_tiles.ensure(tiles.size() * 4));
+  HIPCHK(hipMemcpyAsync(d->s_tiles.p, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice, s));
+  a = a0;
+  a.tiles = d->s_tiles.as<int32_t>();
+  a.ntiles = (int)tiles.size();
+  HIPCHK(fmcw::launch_stft20(a, tab, 1, nullptr, s));
+  CHK(d->stft_tab_done(s));
+  HIPCHK(hipStreamSynchronize(s));   // tiles / cb leave scope
+  d->last_coarse_tiles = (int64_t)tiles.size();
+  if (const char* e = std::getenv("FMCW_STFT_DEBUG"); e && e[0] == '1')
+    std::fprintf(stderr, "stft_coarse_max: nfft %d, %lld segments, %zu of %lld tiles in full\n", nf, (long long)ns,
+                 tiles.size(), (long long)((ns + 255) / 256));
+  return FMCW_OK;
+}
+
 static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, int32_t wlen, int32_t noverlap,
                      int32_t nfft, double fs, int32_t n_log_bins, float* T, float* freq, float* intensity,
                      const char* png_path, int32_t width, int32_t height, int64_t* png_bytes) {
@@ -1370,8 +1424,21 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     int64_t* const d_len = reinterpret_cast<int64_t*>(di + o.len);
     float* const d_win = reinterpret_cast<float*>(di + o.win);
     // the shard's samples are one "frame" of Ld samples in the compaction indirection
-    CHK(fmcw_stft_power_device(d, d_x, d_list, d_len, (int32_t)Ld, nullptr, 0, nullptr, d_win, wlen, noverlap, nf, fs, ns,
-                               sel_mode ? nullptr : d->s_P.as<float>(), d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
+    const char* ce = std::getenv("FMCW_STFT_COARSE");   // 0: every bin of every segment (tests, A/B)
+    const char* me = std::getenv("FMCW_STFT_MFMA");
+    const bool coarse_ok = !(ce && ce[0] == '0') && !(me && me[0] == '0');
+    if (sel_mode && coarse_ok && nf >= (1 << 18)) {   // max(P) only, over a large nfft: coarse-to-fine
+      fmcw::StftArgs a{};
+      a.slow_mag = d_x; a.frame_list = d_list; a.len = d_len; a.pn = (int32_t)Ld;
+      a.win = d_win; a.wlen = wlen; a.hop = hop; a.nfft = nf; a.inv_fs = (float)(1.0 / fs);
+      a.max_seg = ns; a.P = nullptr; a.pmax = d->s_pmax.as<float>(); a.nseg_out = d->s_nseg.as<int64_t>();
+      StageTimer tm(d, 4, s);
+      CHK(stft_coarse_max(d, a, s));
+      tm.done();
+    } else {
+      CHK(fmcw_stft_power_device(d, d_x, d_list, d_len, (int32_t)Ld, nullptr, 0, nullptr, d_win, wlen, noverlap, nf, fs, ns,
+                                 sel_mode ? nullptr : d->s_P.as<float>(), d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
+    }
     if (sel_mode) {   // second pass: P of the listed bins (the W table of the first pass is reused)
       fmcw::StftArgs a{};
       a.slow_mag = d_x; a.frame_list = d_list; a.len = d_len;

@@ -195,13 +195,16 @@ struct StftArgs {
   float* P;                // [max_seg][nfft/2+1]
   float* pmax;
   int64_t* nseg_out;
-  const int32_t* bins;     // k_stft20 mode 3: the ascending bin list of the columns (device), else nullptr
-  int ncol;                // k_stft20 mode 3: columns in `bins`
+  const int32_t* bins;     // k_stft20 mode 3 / 4: the ascending bin list of the columns (device), else nullptr
+  int ncol;                // k_stft20 mode 3 / 4: columns in `bins`
+  const int32_t* tiles;    // k_stft_mfma mode 1: the 256-segment tiles to cover (device), nullptr = all
+  int ntiles;
 };
 
 // 20-tap fast path (kernels_stft.hip k_stft20): W table [nfft/2+1][20] from the window,
 // then mode 0 P + max, 1 max only, 2 dB written to dst (given max), 3 P of the bins
-// a.bins[0..a.ncol) only, written to dst as [seg][ncol]
+// a.bins[0..a.ncol) only, written to dst as [seg][ncol], 4 each segment's max of P over the bins
+// a.bins written to dst[seg] (matrix-core form only)
 bool stft_fast_path(int wlen, int hop);
 hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_t s);
 hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s);

@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
   constexpr int TS = 256, KC = 32;
   typedef float f4t __attribute__((ext_vector_type(4)));
   __shared__ float xs[TS * 4 + STFT_W];
-  __shared__ float tile[MODE == 1 ? 4 : TS * (KC + 1)];
+  __shared__ float tile[MODE == 1 ? 4 : MODE == 4 ? TS : TS * (KC + 1)];   // MODE 4: per-segment max
   __shared__ float bmax[4];
   const int64_t L = *a.len;
   const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
   int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
   if (nseg > a.max_seg) nseg = a.max_seg;
   if (MODE < 2 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
-  const int64_t s0 = (int64_t)blockIdx.x * TS;
+  const int64_t s0 = (int64_t)(a.tiles ? a.tiles[blockIdx.x] : (int)blockIdx.x) * TS;
   if (s0 >= nseg) return;                                           // block-uniform
   const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
   const int nsamp = (ns - 1) * a.hop + STFT_W;
@@ -401,6 +401,7 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
     xs[i] = i >= nsamp ? 0.f : q < L ? a.slow_mag[(int64_t)a.frame_list[q / a.pn] * a.pn + (q % a.pn)] : a.halo[q - L];
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
+  if constexpr (MODE == 4) tile[threadIdx.x] = 0.f;                 // TS == blockDim (P >= 0)
   float u = 0.f;
 #pragma unroll
   for (int m = 0; m < STFT_W; ++m) u = fmaf(tab[m].x, tab[m].x, u);
@@ -411,7 +412,8 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
     inv = pm > 0.f ? 1.0f / pm : 0.f;
   }
   const int nb = a.nfft / 2 + 1;
-  const int ncol = MODE == 3 ? a.ncol : nb;
+  constexpr bool LISTED = MODE == 3 || MODE == 4;
+  const int ncol = LISTED ? a.ncol : nb;
   const int c_lo = blockIdx.y * col_chunk;
   const int c_hi = ncol - c_lo < col_chunk ? ncol : c_lo + col_chunk;
   __syncthreads();
@@ -420,8 +422,8 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
     const int kn = c_hi - k0 < KC ? c_hi - k0 : KC;
     // this lane's two columns of the chunk (col, 16 + col) and their bins
     const bool v0 = col < kn, v1 = 16 + col < kn;
-    const int b0 = v0 ? (MODE == 3 ? a.bins[k0 + col] : k0 + col) : 0;
-    const int b1 = v1 ? (MODE == 3 ? a.bins[k0 + 16 + col] : k0 + 16 + col) : 0;
+    const int b0 = v0 ? (LISTED ? a.bins[k0 + col] : k0 + col) : 0;
+    const int b1 = v1 ? (LISTED ? a.bins[k0 + 16 + col] : k0 + 16 + col) : 0;
     float bw[4][5];
 #pragma unroll
     for (int q = 0; q < 5; ++q) {
@@ -454,6 +456,12 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
           if (v0) lmax = fmaxf(lmax, p0);
           if (v1) lmax = fmaxf(lmax, p1);
         }
+        if constexpr (MODE == 4) {   // the row's 16 lanes hold this segment's columns; one lane owns it
+          float m = fmaxf(v0 ? p0 : 0.f, v1 ? p1 : 0.f);
+#pragma unroll
+          for (int o = 8; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+          if (col == 0 && sl < ns) tile[sl] = fmaxf(tile[sl], m);
+        }
         if constexpr (MODE == 0 || MODE == 3) {
           tile[sl * (KC + 1) + col] = p0;
           tile[sl * (KC + 1) + 16 + col] = p1;
@@ -464,7 +472,7 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
         }
       }
     }
-    if constexpr (MODE != 1) {
+    if constexpr (MODE != 1 && MODE != 4) {
       __syncthreads();
       float* out = MODE == 0 ? a.P : dst;
       for (int i = threadIdx.x; i < ns * kn; i += 256) {            // row-major [seg][col] chunk, coalesced per row
@@ -483,6 +491,10 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
       const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
       max_into(a.pmax, m);
     }
+  }
+  if constexpr (MODE == 4) {
+    __syncthreads();
+    if ((int)threadIdx.x < ns) dst[s0 + threadIdx.x] = tile[threadIdx.x];
   }
 }
 
@@ -619,21 +631,24 @@ hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_
 hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s) {
   if (a.max_seg <= 0) return hipSuccess;
   if (!stft_fast_path(a.wlen, a.hop)) return hipErrorInvalidValue;
-  if (mode == 3 && (!a.bins || a.ncol < 1)) return hipErrorInvalidValue;
-  const int64_t blocks = (a.max_seg + 255) / 256;
+  if ((mode == 3 || mode == 4) && (!a.bins || a.ncol < 1)) return hipErrorInvalidValue;
+  if (a.tiles && (mode != 1 || a.ntiles < 1)) return hipErrorInvalidValue;
+  const int64_t blocks = a.tiles ? a.ntiles : (a.max_seg + 255) / 256;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
   // columns per y-block: enough y-blocks for ~2048 workgroups in all, in chunks of 32 columns
-  const int ncol = mode == 3 ? a.ncol : a.nfft / 2 + 1;
+  // (mode 4 keeps every column of a segment in one block: its per-segment max is block-local)
+  const int ncol = mode == 3 || mode == 4 ? a.ncol : a.nfft / 2 + 1;
   const int64_t chunks = (ncol + 31) / 32;
   int64_t ysplit = (2048 + blocks - 1) / blocks;
   if (ysplit > chunks) ysplit = chunks;
-  if (ysplit < 1) ysplit = 1;
+  if (ysplit < 1 || mode == 4) ysplit = 1;
   const int col_chunk = (int)((chunks + ysplit - 1) / ysplit) * 32;
   const dim3 grid((unsigned)blocks, (unsigned)((ncol + col_chunk - 1) / col_chunk));
   // nfft 64 (config 4): P / max(P) on the matrix cores, bit-identical (FMCW_STFT_MFMA=0: VALU)
   const char* mf = std::getenv("FMCW_STFT_MFMA");
   const float* outp = mode == 0 ? a.P : dst;
-  if (a.nfft == 64 && mode <= 2 && !(mf && mf[0] == '0') && (mode == 1 || (reinterpret_cast<uintptr_t>(outp) & 15) == 0)) {
+  if ((mode == 4 || a.tiles) && mf && mf[0] == '0') return hipErrorInvalidValue;   // matrix-core form only
+  if (a.nfft == 64 && mode <= 2 && !a.tiles && !(mf && mf[0] == '0') && (mode == 1 || (reinterpret_cast<uintptr_t>(outp) & 15) == 0)) {
     if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
     else if (mode == 1) hipLaunchKernelGGL(k_stft64m<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
     else hipLaunchKernelGGL(k_stft64m<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
@@ -643,7 +658,8 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
     if (mode == 0) hipLaunchKernelGGL(k_stft_mfma<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
     else if (mode == 1) hipLaunchKernelGGL(k_stft_mfma<1>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
     else if (mode == 2) hipLaunchKernelGGL(k_stft_mfma<2>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
-    else hipLaunchKernelGGL(k_stft_mfma<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else if (mode == 3) hipLaunchKernelGGL(k_stft_mfma<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else hipLaunchKernelGGL(k_stft_mfma<4>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
     return hipGetLastError();
   }
   if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
