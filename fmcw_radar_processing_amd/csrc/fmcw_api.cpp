@@ -1303,8 +1303,7 @@ static int d2h_big(fmcw_ctx* c, void* dst, const void* d_src, size_t bytes, hipS
 // hold max(P).  Pass 2 takes the max over every bin of the 256-segment tiles that hold a
 // candidate: the same P values the full pass would compare, so the result is the same bits.
 static int stft_coarse_max(fmcw_ctx* d, const fmcw::StftArgs& a0, hipStream_t s) {
-  constexpr int K = 16384;
-  const int nf = a0.nfft, D = nf / K, nc = K / 2 + 1;
+  const int nf = a0.nfft, K = std::min(16384, nf / 8), D = nf / K, nc = K / 2 + 1;   // nf >= 2^16
   const int64_t ns = a0.max_seg;
   std::vector<int32_t> cb(nc);
   for (int m = 0; m < nc; ++m) cb[m] = D * m;
@@ -1427,7 +1426,7 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
     const char* ce = std::getenv("FMCW_STFT_COARSE");   // 0: every bin of every segment (tests, A/B)
     const char* me = std::getenv("FMCW_STFT_MFMA");
     const bool coarse_ok = !(ce && ce[0] == '0') && !(me && me[0] == '0');
-    if (sel_mode && coarse_ok && nf >= (1 << 18)) {   // max(P) only, over a large nfft: coarse-to-fine
+    if (sel_mode && coarse_ok && nf >= (1 << 16)) {   // max(P) only, over a large nfft: coarse-to-fine
       fmcw::StftArgs a{};
       a.slow_mag = d_x; a.frame_list = d_list; a.len = d_len; a.pn = (int32_t)Ld;
       a.win = d_win; a.wlen = wlen; a.hop = hop; a.nfft = nf; a.inv_fs = (float)(1.0 / fs);
