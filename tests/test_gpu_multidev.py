@@ -57,11 +57,12 @@ def test_sharded_process_is_bit_identical(engine, geom, ids):
 
 
 @pytest.mark.parametrize("ids", [[0, 0], [0, 0, 0, 0]])
-@pytest.mark.parametrize("nfft,nbins", [(0, 1024), (64, 0)])
-def test_sharded_stft_is_bit_identical(engine, ids, nfft, nbins):
+@pytest.mark.parametrize("nfft,nbins,L", [(0, 1024, 1333), (64, 0, 1333), (0, 1024, 70_000)],
+                         ids=["ref-rule", "nfft64", "ref-rule-coarse"])   # 70,000: nfft 2^17, coarse max(P) per shard
+def test_sharded_stft_is_bit_identical(engine, ids, nfft, nbins, L):
     cfg, p, wr, wd, cal = case(64, 16, 256, 16, P.PARITY)
     rng = np.random.default_rng(5)
-    x = np.abs(rng.standard_normal(1333)).astype(np.float32) * 100
+    x = np.abs(rng.standard_normal(L)).astype(np.float32) * 100
     x[700:760] *= 50                                           # the global max sits on one shard
     engine.set_taps(cfg, cal, wr, wd)
     win = O.stft_window("kaiser")
