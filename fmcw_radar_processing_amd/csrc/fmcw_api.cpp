@@ -215,67 +215,74 @@ struct fmcw_ctx {
   DevBuf s_P, s_pmax, s_nseg, s_lidx, s_lw, s_out;
   DevBuf s_cbins, s_segmax, s_tiles;   // fmcw_stft's coarse-to-fine max(P) (stft_coarse_max)
   DevBuf r_q, r_nseg, r_img;                   // spectrogram.png render (device 0)
-  // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one: device calls on
-  // different streams (with different windows or nfft) never share a table.  At most kTabs of
-  // them (a caller that passes a fresh stream per call does not grow device memory): the least
-  // recently used one is taken over, and the new stream first waits for the event recorded
-  // behind the old owner's last readers (stft_tab_done), so its rewrite cannot overtake them
-  // -- the event outlives a destroyed stream.
-  struct StreamTab {
-    hipStream_t s = nullptr;
-    DevBuf t;
-    hipEvent_t done = nullptr;
+  // Device scratch kept per stream: device calls on different streams (with different windows,
+  // nfft or frame counts) never share one.  At most kPerStream streams per kind (a caller that
+  // passes a fresh stream per call does not grow device memory): the least recently used entry is
+  // taken over, and the new stream first waits for the event recorded behind the old owner's last
+  // readers (done()), so its rewrite cannot overtake them -- the event outlives a destroyed stream.
+  struct PerStream {
+    struct Entry {
+      hipStream_t s = nullptr;
+      DevBuf t;
+      hipEvent_t done = nullptr;
+      uint64_t tick = 0;
+      ~Entry() {
+        if (done) (void)hipEventDestroy(done);
+      }
+    };
+    static constexpr size_t kPerStream = 8;
+    std::vector<std::unique_ptr<Entry>> es;
     uint64_t tick = 0;
-    ~StreamTab() {
-      if (done) (void)hipEventDestroy(done);
+    void* get(hipStream_t st, size_t bytes, int* status) {
+      Entry* e = nullptr;
+      for (auto& x : es)
+        if (x->s == st) e = x.get();
+      if (!e && es.size() < kPerStream) {
+        es.push_back(std::make_unique<Entry>());
+        e = es.back().get();
+        e->s = st;
+      } else if (!e) {
+        e = es[0].get();
+        for (auto& x : es)
+          if (x->tick < e->tick) e = x.get();
+        if (e->done && hipStreamWaitEvent(st, e->done, 0) != hipSuccess) {
+          (void)hipGetLastError();
+          *status = fail(FMCW_E_HIP, "per-stream scratch: hipStreamWaitEvent failed");
+          return nullptr;
+        }
+        e->s = st;
+      }
+      e->tick = ++tick;
+      *status = e->t.ensure(bytes);
+      return e->t.p;
+    }
+    // after the kernels that read stream st's entry are enqueued
+    int done(hipStream_t st) {
+      for (auto& x : es) {
+        if (x->s != st) continue;
+        if (!x->done && hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
+          (void)hipGetLastError();
+          return fail(FMCW_E_HIP, "per-stream scratch: hipEventCreate failed");
+        }
+        if (hipEventRecord(x->done, st) != hipSuccess) {
+          (void)hipGetLastError();
+          return fail(FMCW_E_HIP, "per-stream scratch: hipEventRecord failed");
+        }
+      }
+      return FMCW_OK;
     }
   };
-  static constexpr size_t kTabs = 8;
-  std::vector<std::unique_ptr<StreamTab>> s_tabs;
-  uint64_t tab_tick = 0;
-  float2* stft_tab(hipStream_t st, size_t bytes, int* status) {
-    StreamTab* e = nullptr;
-    for (auto& x : s_tabs)
-      if (x->s == st) e = x.get();
-    if (!e && s_tabs.size() < kTabs) {
-      s_tabs.push_back(std::make_unique<StreamTab>());
-      e = s_tabs.back().get();
-      e->s = st;
-    } else if (!e) {
-      e = s_tabs[0].get();
-      for (auto& x : s_tabs)
-        if (x->tick < e->tick) e = x.get();
-      if (e->done && hipStreamWaitEvent(st, e->done, 0) != hipSuccess) {
-        (void)hipGetLastError();
-        *status = fail(FMCW_E_HIP, "STFT table: hipStreamWaitEvent failed");
-        return nullptr;
-      }
-      e->s = st;
-    }
-    e->tick = ++tab_tick;
-    *status = e->t.ensure(bytes);
-    return e->t.as<float2>();
-  }
-  // after the kernels that read stream st's table are enqueued
-  int stft_tab_done(hipStream_t st) {
-    for (auto& x : s_tabs) {
-      if (x->s != st) continue;
-      if (!x->done && hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(FMCW_E_HIP, "STFT table: hipEventCreate failed");
-      }
-      if (hipEventRecord(x->done, st) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(FMCW_E_HIP, "STFT table: hipEventRecord failed");
-      }
-    }
-    return FMCW_OK;
-  }
+  // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one
+  PerStream s_tabs;
+  float2* stft_tab(hipStream_t st, size_t bytes, int* status) { return static_cast<float2*>(s_tabs.get(st, bytes, status)); }
+  int stft_tab_done(hipStream_t st) { return s_tabs.done(st); }
+  // K1's per-workgroup profile maxima of fmcw_range_fft_device (config 2), one per stream: two
+  // range-only calls on different streams of one context do not write over each other's partials
+  PerStream k1_part;
   int64_t chunk_frames = 0;
   int64_t last_coarse_tiles = -1;     // tiles the last coarse-to-fine max(P) evaluated in full (diagnostics)
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
-  DevBuf k1_part;                               // K1's per-workgroup profile maxima (range-only calls)
   DevBuf x_cube, x_ctr, x_err, x_tab;          // XCD-team schedule: hand-off slots, counters, sticky error, XT_* table
   int xcd_teams = -1;                          // census of the device: its XCD teams (-1 not run yet, 0 none)
   int8_t xcc_team[16] = {};                    // HW_REG_XCC_ID -> team
@@ -1052,12 +1059,16 @@ int fmcw_range_fft_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, i
   const int64_t per_wg = (int64_t)teams * cpt;
   ra.parts = (per_wg < p->pn && p->pn % per_wg == 0) ? (int)(p->pn / per_wg) : 0;
   if (ra.parts > 1) {
-    CHK(c->k1_part.ensure((size_t)F * ra.parts * p->nr * 4));
-    ra.prof_part = c->k1_part.as<float>();
+    int st = FMCW_OK;
+    ra.prof_part = static_cast<float*>(c->k1_part.get(s, (size_t)F * ra.parts * p->nr * 4, &st));
+    CHK(st);
   }
   StageTimer tm(c, 6, s);
   HIPCHK(fmcw::launch_range(ra, s));
-  if (ra.parts > 1) HIPCHK(fmcw::launch_profile_reduce(ra.prof_part, ra.parts, F, p->nr, d_prof, s));
+  if (ra.parts > 1) {
+    HIPCHK(fmcw::launch_profile_reduce(ra.prof_part, ra.parts, F, p->nr, d_prof, s));
+    CHK(c->k1_part.done(s));
+  }
   tm.done();
   return FMCW_OK;
 }
@@ -1113,7 +1124,9 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
     float2* tab = c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
     CHK(st);
     HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
-    HIPCHK(fmcw::launch_stft20(a, tab, d_P ? 0 : 1, nullptr, s));
+    // device API: d_P is the caller's [max_seg][nfft/2+1] (fmcw.h), the table this stream's
+    HIPCHK(fmcw::launch_stft20(a, tab, d_P ? 0 : 1, nullptr, s, max_seg * (int64_t)(nfft / 2 + 1),
+                               (int64_t)(nfft / 2 + 1) * 20));
     CHK(c->stft_tab_done(s));
   } else {
     HIPCHK(fmcw::launch_stft_power(a, s));
@@ -1148,7 +1161,7 @@ int fmcw_stft_db_direct_device(fmcw_ctx* c, const float* d_slow, const int32_t* 
   float2* tab = c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
   CHK(st);
   HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
-  HIPCHK(fmcw::launch_stft20(a, tab, 2, d_out, s));
+  HIPCHK(fmcw::launch_stft20(a, tab, 2, d_out, s, max_seg * (int64_t)(nfft / 2 + 1), (int64_t)(nfft / 2 + 1) * 20));
   CHK(c->stft_tab_done(s));
   tm.done();
   return FMCW_OK;
@@ -1303,8 +1316,14 @@ static int d2h_big(fmcw_ctx* c, void* dst, const void* d_src, size_t bytes, hipS
 // hold max(P).  Pass 2 takes the max over every bin of the 256-segment tiles that hold a
 // candidate: the same P values the full pass would compare, so the result is the same bits.
 static int stft_coarse_max(fmcw_ctx* d, const fmcw::StftArgs& a0, hipStream_t s) {
+  // The bound below holds for the 20-tap window only (a degree-19 trigonometric polynomial per
+  // segment; any sign of the samples) and for a power-of-two nfft of at least 2^16, so that the
+  // coarse grid (every D-th bin) holds DC, Nyquist and an interior bin within h of any peak.
+  if (!fmcw::stft_fast_path(a0.wlen, a0.hop)) return fail(FMCW_E_ARG, "stft_coarse_max: not the 20-tap fast path");
+  if (a0.nfft < (1 << 16) || (a0.nfft & (a0.nfft - 1))) return fail(FMCW_E_ARG, "stft_coarse_max: nfft must be a power of two >= 2^16");
   const int nf = a0.nfft, K = std::min(16384, nf / 8), D = nf / K, nc = K / 2 + 1;   // nf >= 2^16
   const int64_t ns = a0.max_seg;
+  if (ns < 1 || ns > 0x7fffffffLL) return fail(FMCW_E_ARG, "stft_coarse_max: bad segment count");
   std::vector<int32_t> cb(nc);
   for (int m = 0; m < nc; ++m) cb[m] = D * m;
   CHK(d->s_cbins.ensure((size_t)nc * 4));
@@ -1317,7 +1336,9 @@ static int stft_coarse_max(fmcw_ctx* d, const fmcw::StftArgs& a0, hipStream_t s)
   fmcw::StftArgs a = a0;
   a.bins = d->s_cbins.as<int32_t>();
   a.ncol = nc;
-  HIPCHK(fmcw::launch_stft20(a, tab, 4, d->s_segmax.as<float>(), s));
+  // mode 4 writes one float per segment: s_segmax holds ns (launch_stft20 checks the capacity)
+  HIPCHK(fmcw::launch_stft20(a, tab, 4, d->s_segmax.as<float>(), s, (int64_t)(d->s_segmax.n / 4),
+                             (int64_t)(nf / 2 + 1) * 20));
   std::vector<float> sm((size_t)ns);
   HIPCHK(hipMemcpyAsync(sm.data(), d->s_segmax.p, (size_t)ns * 4, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
@@ -1336,7 +1357,7 @@ static int stft_coarse_max(fmcw_ctx* d, const fmcw::StftArgs& a0, hipStream_t s)
   a = a0;
   a.tiles = d->s_tiles.as<int32_t>();
   a.ntiles = (int)tiles.size();
-  HIPCHK(fmcw::launch_stft20(a, tab, 1, nullptr, s));
+  HIPCHK(fmcw::launch_stft20(a, tab, 1, nullptr, s, 0, (int64_t)(nf / 2 + 1) * 20));
   CHK(d->stft_tab_done(s));
   HIPCHK(hipStreamSynchronize(s));   // tiles / cb leave scope
   d->last_coarse_tiles = (int64_t)tiles.size();
@@ -1447,7 +1468,7 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       int st = FMCW_OK;
       float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table on s
       CHK(st);
-      HIPCHK(fmcw::launch_stft20(a, tab, 3, d->s_P.as<float>(), s));
+      HIPCHK(fmcw::launch_stft20(a, tab, 3, d->s_P.as<float>(), s, (int64_t)(d->s_P.n / 4), (int64_t)(nf / 2 + 1) * 20));
       CHK(d->stft_tab_done(s));
       tm.done();
     }

@@ -207,7 +207,10 @@ struct StftArgs {
 // a.bins written to dst[seg] (matrix-core form only)
 bool stft_fast_path(int wlen, int hop);
 hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_t s);
-hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s);
+// dst_cap: floats available at dst (mode 0: at a.P), tab_cap: float2 entries of tab; a launch
+// whose writes would not fit returns hipErrorInvalidValue before anything is enqueued
+hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s, int64_t dst_cap,
+                         int64_t tab_cap);
 
 struct StftDbArgs {
   const float* P;

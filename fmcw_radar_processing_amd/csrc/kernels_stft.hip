@@ -529,7 +529,7 @@ __global__ __launch_bounds__(256) void k_stft_db_flat(StftDbArgs a) {
   const float inv = pm > 0.f ? 1.0f / pm : 0.f;
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const f4t* __restrict__ in = reinterpret_cast<const f4t*>(a.P);
+  const f4t* in = reinterpret_cast<const f4t*>(a.P);          // not __restrict__: P and out may alias
   f4t* out = reinterpret_cast<f4t*>(a.out);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const f4t v = in[i];
@@ -628,13 +628,23 @@ hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_
   return hipGetLastError();
 }
 
-hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s) {
+hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s, int64_t dst_cap,
+                         int64_t tab_cap) {
   if (a.max_seg <= 0) return hipSuccess;
+  if (mode < 0 || mode > 4 || !tab) return hipErrorInvalidValue;
   if (!stft_fast_path(a.wlen, a.hop)) return hipErrorInvalidValue;
   if ((mode == 3 || mode == 4) && (!a.bins || a.ncol < 1)) return hipErrorInvalidValue;
   if (a.tiles && (mode != 1 || a.ntiles < 1)) return hipErrorInvalidValue;
   const int64_t blocks = a.tiles ? a.ntiles : (a.max_seg + 255) / 256;
   if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+  // What each mode writes, against the capacity the caller states (round 4's GPU fault: a mode-4
+  // launch that reached the mode-3 kernel writes [seg][ncol] P columns into the [seg] maxima,
+  // DESIGN.md 4.0.2): 0 P [max_seg][nb] at a.P, 2 dB [max_seg][nb] at dst, 3 P [max_seg][ncol]
+  // at dst, 4 one maximum per segment at dst; 1 only max(P).  The W table is [nfft/2+1][20].
+  const int64_t nb = a.nfft / 2 + 1;
+  if (tab_cap < nb * STFT_W) return hipErrorInvalidValue;
+  const int64_t need = mode == 0 || mode == 2 ? a.max_seg * nb : mode == 3 ? a.max_seg * a.ncol : mode == 4 ? a.max_seg : 0;
+  if (need > 0 && ((mode == 0 ? !a.P : !dst) || dst_cap < need)) return hipErrorInvalidValue;
   // columns per y-block: enough y-blocks for ~2048 workgroups in all, in chunks of 32 columns
   // (mode 4 keeps every column of a segment in one block: its per-segment max is block-local)
   const int ncol = mode == 3 || mode == 4 ? a.ncol : a.nfft / 2 + 1;
@@ -659,13 +669,15 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
     else if (mode == 1) hipLaunchKernelGGL(k_stft_mfma<1>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
     else if (mode == 2) hipLaunchKernelGGL(k_stft_mfma<2>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
     else if (mode == 3) hipLaunchKernelGGL(k_stft_mfma<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
-    else hipLaunchKernelGGL(k_stft_mfma<4>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else if (mode == 4) hipLaunchKernelGGL(k_stft_mfma<4>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
   }
   if (mode == 0) hipLaunchKernelGGL(k_stft20<0>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
   else if (mode == 1) hipLaunchKernelGGL(k_stft20<1>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
   else if (mode == 2) hipLaunchKernelGGL(k_stft20<2>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
-  else hipLaunchKernelGGL(k_stft20<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+  else if (mode == 3) hipLaunchKernelGGL(k_stft20<3>, grid, dim3(256), 0, s, a, tab, dst, col_chunk);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -21,6 +21,7 @@ The blob uploads are a caller-supplied hook (``upload``, default: none).
 from __future__ import annotations
 
 import os
+import threading
 from typing import Callable
 
 import numpy as np
@@ -135,27 +136,40 @@ def write_outputs_no(out_dir: str, filename: str, cfg: P.FmcwConfig, per: dict, 
 # the entry point (GPU)
 # ---------------------------------------------------------------------------
 _DEFAULT_ENGINE = None
+_DEFAULT_DEVICES_ENV = None
+# The default context is not reentrant: libfmcw's context shares pinned staging, scratch and STFT
+# tables between calls, and ctypes releases the GIL inside the library.  Calls that pass no engine
+# therefore hold this lock for the whole call (threads that want concurrency pass engines of their
+# own, one per thread, as the MEX gateway keeps one context per MATLAB worker process).
+_DEFAULT_LOCK = threading.RLock()
 
 
 def _default_engine():
     """The per-process context of calls that pass no engine, created once (as the MEX gateway's
     static context: mexLock on create, mexAtExit destroy).  Devices: FMCW_DEVICES when it is set
-    (fmcw_default_devices), else GPU 0 only -- a deployed 115-frame file does not pay for a
-    context and an RCCL communicator on every GPU of the node, and takes no GPU it was not given."""
-    global _DEFAULT_ENGINE
+    (fmcw_default_devices, the rule the MEX gateway uses), else GPU 0 only -- a deployed 115-frame
+    file does not pay for a context and an RCCL communicator on every GPU of the node, and takes no
+    GPU it was not given.  A change of FMCW_DEVICES between calls re-creates the context.
+    Call with _DEFAULT_LOCK held."""
+    global _DEFAULT_ENGINE, _DEFAULT_DEVICES_ENV
+    env = os.environ.get("FMCW_DEVICES")
+    if _DEFAULT_ENGINE is not None and env != _DEFAULT_DEVICES_ENV:
+        _drop_default_engine()
     if _DEFAULT_ENGINE is None:
         import atexit
         from .engine import Engine
-        _DEFAULT_ENGINE = Engine(None if os.environ.get("FMCW_DEVICES") else 0)
+        _DEFAULT_ENGINE = Engine(None if env else 0)
+        _DEFAULT_DEVICES_ENV = env
         atexit.register(_drop_default_engine)
     return _DEFAULT_ENGINE
 
 
 def _drop_default_engine():
     global _DEFAULT_ENGINE
-    eng, _DEFAULT_ENGINE = _DEFAULT_ENGINE, None
-    if eng is not None:
-        eng.close()
+    with _DEFAULT_LOCK:
+        eng, _DEFAULT_ENGINE = _DEFAULT_ENGINE, None
+        if eng is not None:
+            eng.close()
 
 
 def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_data: np.ndarray,
@@ -174,8 +188,15 @@ def radar_processing(process_animal_activity: str, *, frames: np.ndarray, calib_
     cfg = P.derive_params(device, nr=nr, nd=nd, mode=mode)             # :89-154
     cal = P.calibration(calib_data, cfg.n_rx, cfg.nts)                 # :166-174
     frames = np.asarray(frames)
+    if engine is None:                                                 # the shared default context:
+        with _DEFAULT_LOCK:                                            # one call at a time
+            return _radar_processing(process_animal_activity, frames, cfg, cal, filename, out_dir,
+                                     _default_engine(), upload)        # FMCW_DEVICES, else GPU 0
+    return _radar_processing(process_animal_activity, frames, cfg, cal, filename, out_dir, engine, upload)
+
+
+def _radar_processing(process_animal_activity, frames, cfg, cal, filename, out_dir, eng, upload):
     F = frames.shape[0]
-    eng = _default_engine() if engine is None else engine              # FMCW_DEVICES, else GPU 0
     eng.set_taps(cfg, cal)                                             # :138-139 windows
     flag = str(process_animal_activity).lower()
     if flag == "no":

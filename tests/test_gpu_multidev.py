@@ -116,9 +116,10 @@ def test_rccl_context_over_distinct_devices(engine):
 
 
 def test_default_devices_drive_every_gpu(engine, monkeypatch):
-    """fmcw_default_devices (the drop-in's choice: matlab/radar_processing.m fmcw_mex('init'),
-    radar.radar_processing with no engine): every visible GPU unless FMCW_DEVICES names some;
-    a context over them gives the one-device results."""
+    """fmcw_default_devices (the MEX drop-in's choice: matlab/radar_processing.m fmcw_mex('init')):
+    every visible GPU unless FMCW_DEVICES names some; a context over them gives the one-device
+    results.  (radar.radar_processing with no engine takes this rule only when FMCW_DEVICES is
+    set, else GPU 0: radar._default_engine.)"""
     from fmcw_radar_processing_amd.engine import default_devices
     monkeypatch.delenv("FMCW_DEVICES", raising=False)
     assert default_devices() == list(range(_n_gpus()))
