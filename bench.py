@@ -123,18 +123,69 @@ def apply_stream_frames(args, world: int) -> None:
 
 
 def dry_dist(args, world: int, rank: int) -> None:
-    """The launcher path on CPU (tests/test_bench_harness.py): ranks meet over gloo; rank 0
-    prints the config block the GPU run would carry."""
+    """The launcher path and the step's collectives on CPU (tests/test_bench_harness.py): the ranks
+    meet over gloo and run, for every one of the run's steps, exactly the exchange sequence of
+    step() (exchange_halo -> the max(P) all_reduce of the STFT leg -> exchange_rows) on CPU tensors
+    of the step's shapes (--frames frames of 256 chirps per rank), standing in for the device
+    outputs; each rank checks what it received against what every rank must have sent (the
+    inputs are seeded by global frame index), and rank 0 prints the config block the GPU run
+    would carry."""
+    import numpy as np
     import torch
     import torch.distributed as dist
+
+    from fmcw_radar_processing_amd import dist as fdist
     dist.init_process_group("gloo")
     t = torch.ones(1)
     dist.all_reduce(t)
+    F, C, h, M = args.frames, 256, STFT_WLEN - 1, 1
+
+    def shard(r, step):                 # what rank r's device outputs would hold at this step
+        g = np.random.default_rng(1000003 * step + r)
+        cnt = (g.random(F) < 0.9).astype(np.int32)
+        if r == 1 and step == 0:
+            cnt[:] = 0                  # an empty slow-time shard: the halo must skip it
+        slow = (g.random((F, C)) * 40).astype(np.float32) * cnt[:, None]
+        ridx = (g.integers(2, 30, (F, M)) * cnt[:, None]).astype(np.int32)
+        didx = (g.integers(1, 257, (F, M)) * cnt[:, None]).astype(np.int32)
+        rmag = (g.random((F, M)) * 500).astype(np.float32) * cnt[:, None]
+        keep = np.nonzero(cnt)[0]
+        return cnt, slow, ridx, didx, rmag, keep
+
+    checks = {"steps": 0, "halo": True, "lengths": True, "max": True, "rows": True}
+    for step in range(args.steps):
+        cnt, slow, ridx, didx, rmag, keep = shard(rank, step)
+        outs = {"tgt_count": torch.from_numpy(cnt), "slow_mag": torch.from_numpy(slow),
+                "tgt_range_idx": torch.from_numpy(ridx), "tgt_doppler_idx": torch.from_numpy(didx),
+                "tgt_range_mag": torch.from_numpy(rmag)}
+        flist = torch.zeros(F, dtype=torch.int32)
+        flist[: len(keep)] = torch.from_numpy(keep.astype(np.int32))
+        d_len = torch.tensor([len(keep) * C], dtype=torch.int64)
+        hbuf, hl = exchange_halo(fdist, world, rank, outs, flist, d_len, h)
+        pmax = torch.tensor([float(slow.max()) if len(keep) else 0.0])       # stands in for pass 1's max(P)
+        fdist.global_max_(pmax)
+        rows = exchange_rows(fdist, world, outs)
+        # what the exchange must deliver, from every rank's seeded shard
+        allsh = [shard(r, step) for r in range(world)]
+        nxt = np.concatenate([a[1][a[5]].reshape(-1) for a in allsh[rank + 1:]] + [np.zeros(0, np.float32)])[:h]
+        checks["halo"] &= int(hl.item()) == len(nxt) and np.array_equal(hbuf.numpy()[: len(nxt)], nxt)
+        checks["max"] &= float(pmax.item()) == max(float(a[1].max()) if len(a[5]) else 0.0 for a in allsh)
+        checks["lengths"] &= int(fdist.all_lengths(d_len).sum().item()) == C * sum(len(a[5]) for a in allsh)
+        if rank == 0:
+            want = np.concatenate([np.concatenate([a[0].reshape(-1, 1).astype(np.float32), a[2], a[3], a[4]], 1)
+                                   for a in allsh], 0)
+            checks["rows"] &= rows is not None and np.array_equal(rows.numpy(), want)
+        checks["steps"] += 1
+    ok = torch.tensor([int(all(v for k, v in checks.items() if k != "steps"))])
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if rank == 0:
         print(json.dumps({"metric": METRIC, "n_gpus": world, "ranks_reduced": int(t.item()), "dry_dist": True,
-                          "steps": args.steps, "config": config_block(world, args.frames, args.steps)}),
+                          "steps": args.steps, "exchange": {**checks, "all_ranks_ok": bool(ok.item())},
+                          "config": config_block(world, args.frames, args.steps)}),
               flush=True)
     dist.destroy_process_group()
+    if not ok.item():
+        sys.exit(4)
 
 
 def main():
@@ -202,18 +253,12 @@ def main():
     halo_len = torch.zeros(1, dtype=torch.int64, device=dev)
 
     def step():
-        eng.process_device(d_iq, F, dt, outs, d_rd=d_rd, out_dtype=dt, stream=stream)
-        eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
-        hl, hbuf = None, None
-        if world > 1:
-            lens = fdist.all_lengths(d_len)
-            head = fdist.head_samples(outs["slow_mag"], flist, d_len, h)
-            hbuf, hl = fdist.right_halo(head, lens, rank)
+        # per-frame stages + the slow-time leg's start (compaction, max(P) reset) in one call
+        eng.process_slow_device(d_iq, F, dt, outs, flist, d_len, d_pmax=pmax, d_rd=d_rd, out_dtype=dt, stream=stream)
+        hbuf, hl = exchange_halo(fdist, world, rank, outs, flist, d_len, h)
         stft_leg(eng, args.stft_form, outs["slow_mag"], flist, d_len, C, win, fs, max_seg, d_P, pmax, nseg,
                  hbuf, hl, h if world > 1 else 0, fdist.global_max_ if world > 1 else None, stream)
-        if world > 1:
-            fdist.gather_range_speed(outs["tgt_count"], outs["tgt_range_idx"], outs["tgt_doppler_idx"],
-                                     outs["tgt_range_mag"])
+        exchange_rows(fdist, world, outs)
 
     def barrier():
         if world > 1:
@@ -365,12 +410,32 @@ def main():
         sys.exit(1)
 
 
+def exchange_halo(fdist, world, rank, outs, flist, d_len, h):
+    """The step's collectives before the STFT (dist.py): every shard's compacted
+    length, then the right halo -- the first wlen-1 samples of the following shards.  (None, None)
+    on one GPU.  The same calls run over gloo on CPU tensors in --dry-dist."""
+    if world == 1:
+        return None, None
+    lens = fdist.all_lengths(d_len)
+    head = fdist.head_samples(outs["slow_mag"], flist, d_len, h)
+    return fdist.right_halo(head, lens, rank)
+
+
+def exchange_rows(fdist, world, outs):
+    """The step's collective after the STFT: the per-frame range_speed rows
+    gathered to rank 0 (:386-389).  Returns them on rank 0, None elsewhere or on one GPU."""
+    if world == 1:
+        return None
+    return fdist.gather_range_speed(outs["tgt_count"], outs["tgt_range_idx"], outs["tgt_doppler_idx"],
+                                    outs["tgt_range_mag"])
+
+
 def stft_leg(eng, form, slow, flist, d_len, C, win, fs, max_seg, d_P, pmax, nseg, hbuf, hl, n_halo, gmax, stream):
     """The STFT leg of a step (:270-283) over the compacted slow-time rows; d_P ends as the dB map.
     stored: pass 1 writes P (:276) and max(P), pass 2 turns P into 20 log10(P / max) in place;
     direct: pass 1 forms max(P) only, pass 2 recomputes P and writes the dB.  gmax: the
-    all_reduce(MAX) of max(P) across ranks (dist.py), between the passes."""
-    pmax.zero_()
+    all_reduce(MAX) of max(P) across ranks (dist.py), between the passes.  pmax was zeroed by the
+    step's process_slow_device call (the detection kernel's last workgroup)."""
     stored = form == "stored"
     eng.stft_power_device(slow, flist, d_len, C, win, STFT_WLEN, STFT_NOVERLAP, STFT_NFFT, fs, max_seg,
                           d_P if stored else None, pmax, nseg, d_halo=hbuf, n_halo=n_halo, d_halo_len=hl,
@@ -462,8 +527,8 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     eng.set_pipeline({"auto": 0, "streams": 1, "onepass": 3, "xcd": 4}[args.pipeline])
 
     def step():
-        eng.process_device(d_iq, F, FMCW_C32H, outs, d_rd=d_rd, out_dtype=FMCW_C32H, stream=stream)
-        eng.compact_device(outs["tgt_count"], F, flist, d_len, stream=stream)
+        eng.process_slow_device(d_iq, F, FMCW_C32H, outs, flist, d_len, d_pmax=pmax, d_rd=d_rd, out_dtype=FMCW_C32H,
+                                stream=stream)
         stft_leg(eng, args.stft_form, outs["slow_mag"], flist, d_len, C, win, fs, max_seg, d_P, pmax, nseg,
                  None, None, 0, None, stream)
 

@@ -17,7 +17,7 @@ FMCW_OK = 0
 FMCW_E_ARG, FMCW_E_HIP, FMCW_E_OOM, FMCW_E_STATE, FMCW_E_DATA = -1, -2, -3, -4, -5
 FMCW_C64, FMCW_C32H = 0, 1
 FMCW_PIPE_AUTO, FMCW_PIPE_STREAMS, FMCW_PIPE_ONEPASS, FMCW_PIPE_XCD = 0, 1, 3, 4
-ABI_VERSION = 3
+ABI_VERSION = 4
 STATUS_NAMES = {0: "OK", -1: "E_ARG", -2: "E_HIP", -3: "E_OOM", -4: "E_STATE", -5: "E_DATA"}
 STAGES = ("range", "doppler", "detect", "compact", "stft_power", "stft_db", "range_only", "range_doppler", "onepass",
           "render")
@@ -69,6 +69,8 @@ SIGNATURES = {
     "fmcw_process_device": (ct.c_int, [_P, _PP, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _I32, _I64,
                                        _P, _P]),
     "fmcw_range_fft_device": (ct.c_int, [_P, _PP, _P, _I32, _I64, _P, _I32, _P, _P]),
+    "fmcw_process_slow_device": (ct.c_int, [_P, _PP, _P, _I32, _I64, _P, _P, _P, _P, _P, _P, _P, _I32, _P, _P, _P,
+                                            _P]),
     "fmcw_compact_device": (ct.c_int, [_P, _P, _I64, _I32, _P, _P, _P]),
     "fmcw_stft_power_device": (ct.c_int, [_P, _P, _P, _P, _I32, _P, _I32, _P, _P, _I32, _I32, _I32, _D, _I64,
                                           _P, _P, _P, _P]),

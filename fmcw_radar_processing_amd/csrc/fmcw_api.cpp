@@ -226,6 +226,8 @@ struct fmcw_ctx {
       DevBuf t;
       hipEvent_t done = nullptr;
       uint64_t tick = 0;
+      const void* key = nullptr;   // what the contents were built from (STFT tables: the window pointer)
+      int64_t key_n = 0;           // and its size (the nfft)
       ~Entry() {
         if (done) (void)hipEventDestroy(done);
       }
@@ -233,7 +235,7 @@ struct fmcw_ctx {
     static constexpr size_t kPerStream = 8;
     std::vector<std::unique_ptr<Entry>> es;
     uint64_t tick = 0;
-    void* get(hipStream_t st, size_t bytes, int* status) {
+    void* get(hipStream_t st, size_t bytes, int* status, bool* fresh = nullptr) {
       Entry* e = nullptr;
       for (auto& x : es)
         if (x->s == st) e = x.get();
@@ -251,11 +253,21 @@ struct fmcw_ctx {
           return nullptr;
         }
         e->s = st;
+        e->key = nullptr;
+        e->key_n = 0;
       }
       e->tick = ++tick;
+      void* before = e->t.p;
       *status = e->t.ensure(bytes);
+      if (e->t.p != before) {                  // newly allocated: its contents are undefined
+        e->key = nullptr;
+        e->key_n = 0;
+      }
+      if (fresh) *fresh = e->t.p != before;
+      last = e;
       return e->t.p;
     }
+    Entry* last = nullptr;                     // the entry the last get() returned
     // after the kernels that read stream st's entry are enqueued
     int done(hipStream_t st) {
       for (auto& x : es) {
@@ -272,17 +284,38 @@ struct fmcw_ctx {
       return FMCW_OK;
     }
   };
-  // STFT 20-tap tables W[nfft/2+1][20], one per stream that asked for one
+  // STFT 20-tap tables W[nfft/2+1][20] + the 20 taps they were built from, one per stream that
+  // asked for one
   PerStream s_tabs;
-  float2* stft_tab(hipStream_t st, size_t bytes, int* status) { return static_cast<float2*>(s_tabs.get(st, bytes, status)); }
+  float2* stft_tab(hipStream_t st, size_t bytes, int* status) {
+    return static_cast<float2*>(s_tabs.get(st, bytes + STFT_TAPS_BYTES, status));
+  }
+  static constexpr size_t STFT_TAPS_BYTES = 20 * 4;
+  // The device calls at nfft 64 (the bench's config-4 STFT, two passes per step) keep the
+  // stream's table while the window pointer and nfft are unchanged: k_stft64m compares the 20
+  // taps stored behind the table with the call's window and forms its W entries itself when they
+  // differ (a window rewritten in place), so the table is rebuilt once, not every pass.
+  // *build: the caller must launch k_stft_table into the returned table.
+  float2* stft_tab64(hipStream_t st, const float* d_win, int nfft, bool* build, int* status) {
+    float2* t = stft_tab(st, (size_t)(nfft / 2 + 1) * 20 * 8, status);
+    if (!t) return nullptr;
+    PerStream::Entry* e = s_tabs.last;
+    *build = !(e->key == d_win && e->key_n == nfft);
+    e->key = d_win;
+    e->key_n = nfft;
+    return t;
+  }
   int stft_tab_done(hipStream_t st) { return s_tabs.done(st); }
   // K1's per-workgroup profile maxima of fmcw_range_fft_device (config 2), one per stream: two
   // range-only calls on different streams of one context do not write over each other's partials
   PerStream k1_part;
+  // k_detect_1p's arrival counter of the fused compaction (fmcw_process_slow_device), one per
+  // stream; zeroed when allocated, reset by the kernel's last workgroup
+  PerStream det_done;
   int64_t chunk_frames = 0;
   int64_t last_coarse_tiles = -1;     // tiles the last coarse-to-fine max(P) evaluated in full (diagnostics)
   int pipe_mode = FMCW_PIPE_AUTO;
-  DevBuf op_rowpk, op_cidx, op_crows, op_fix;   // single-pass schedule scratch (per chunk)
+  DevBuf op_rowpk, op_cidx, op_crows;           // single-pass schedule scratch (per chunk)
   DevBuf x_cube, x_ctr, x_err, x_tab;          // XCD-team schedule: hand-off slots, counters, sticky error, XT_* table
   int xcd_teams = -1;                          // census of the device: its XCD teams (-1 not run yet, 0 none)
   int8_t xcc_team[16] = {};                    // HW_REG_XCC_ID -> team
@@ -747,15 +780,23 @@ static unsigned host_s16mask(const fmcw_params* p, int NR) {
   return m;
 }
 
+// The slow-time leg's start, fused into the detection (fmcw_process_slow_device): the
+// compaction of :257-260 (frame list, L) and the reset of the STFT's running max(P).
+struct SlowLeg {
+  int32_t* list;
+  int64_t* len;
+  float* pmax;   // may be NULL
+};
+
 // Single-pass schedule (kernels_xcd.hip): k_rdx computes range FFT, profile,
 // Doppler FFT and the slow-time candidate rows of each frame, the range cube
-// handed between the CUs of one XCD; k_detect_1p runs the detection; k_slow_fix
-// recomputes the rare slow-time row that was not among a group's candidates.
+// handed between the CUs of one XCD; k_detect_1p runs the detection (and
+// recomputes the rare slow-time row that was not among a group's candidates).
 // Chunks bound the candidate scratch (XCD_TILES * XCD_CAND rows of PN floats per
 // frame).  The hand-off ring has XCD_MAX_SLOTS slots per XCD.
 static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int h, int64_t F, float* d_prof,
                            int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx, float* d_slow,
-                           void* d_rd, int64_t probe_column, float* d_probe, hipStream_t s) {
+                           void* d_rd, int64_t probe_column, float* d_probe, const SlowLeg* leg, hipStream_t s) {
   const int C = p->pn, S = p->nts, NR = p->nr, ND = p->nd, M = p->max_targets;
   const int64_t chunk = std::min<int64_t>(F, c->chunk_frames > 0 ? c->chunk_frames : 8192);
   const int tiles = fmcw::XCD_TILES, ncand = fmcw::XCD_CAND;
@@ -772,9 +813,14 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   CHK(c->op_rowpk.ensure((size_t)chunk * NR * 8));
   CHK(c->op_cidx.ensure((size_t)chunk * TC * 4));
   CHK(c->op_crows.ensure((size_t)chunk * TC * C * 4));
-  CHK(c->op_fix.ensure((size_t)chunk * 4 + 16));
-  int32_t* fix_count = c->op_fix.as<int32_t>();
-  int32_t* fix_list = fix_count + 4;
+  int32_t* det_done = nullptr;
+  if (leg) {
+    int st = FMCW_OK;
+    bool fresh = false;
+    det_done = static_cast<int32_t*>(c->det_done.get(s, 4, &st, &fresh));
+    CHK(st);
+    if (fresh) HIPCHK(hipMemsetAsync(det_done, 0, 4, s));
+  }
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
   const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;
   if (!c->x_tab_ok) CHK(build_xcd_tab(c, s));
@@ -846,7 +892,6 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       }
       tm.done();
     }
-    HIPCHK(hipMemsetAsync(fix_count, 0, 4, s));
     fmcw::Detect1pArgs k{};
     k.profile = a.profile; k.rowpk = a.rowpk; k.rd = a.rd; k.ND = ND; k.rd_h = h; k.cand_idx = a.cand_idx; k.cand_rows = a.cand_rows;
     k.tiles = tiles; k.ncand = ncand;
@@ -858,28 +903,56 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     k.det.cube_unscale = 1.0f; k.det.rd_unscale = 1.0f / a.rd_scale;
     k.count = d_count + f0; k.ridx = d_ridx + f0 * M; k.rmag = d_rmag + f0 * M; k.didx = d_didx + f0 * M;
     k.slow_mag = d_slow + f0 * C;
-    k.fix_list = fix_list; k.fix_count = fix_count;
+    k.iq = a.iq; k.h = h; k.S = S; k.calw = a.calw; k.tw_nr = a.tw_nr;
+    if (leg && f0 + nf == F) {   // the last chunk's detection also compacts every frame of the call
+      k.done = det_done; k.count_all = d_count; k.F_all = F; k.pn = C;
+      k.list = leg->list; k.len = leg->len; k.pmax_reset = leg->pmax;
+    }
     {
       StageTimer tm(c, 2, s, 2);
       HIPCHK(fmcw::launch_detect_1p(k, s));
       tm.done();
     }
-    fmcw::SlowFixArgs x{};
-    x.iq = a.iq; x.h = h; x.C = C; x.S = S; x.NR = NR;
-    x.calw = a.calw; x.tw_nr = a.tw_nr;
-    x.ridx = k.ridx; x.M = M;
-    x.fix_list = fix_list; x.fix_count = fix_count;
-    x.slow_mag = k.slow_mag;
-    HIPCHK(fmcw::launch_slow_fix(x, s));
   }
+  if (leg) CHK(c->det_done.done(s));
   span.done();
   return FMCW_OK;
 }
+
+static int process_device_impl(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
+                               float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
+                               float* d_slow, void* d_cube, void* d_rd, int32_t out_dtype, int64_t probe_column,
+                               float* d_probe, const SlowLeg* leg, void* stream);
 
 int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
                         float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
                         float* d_slow, void* d_cube, void* d_rd, int32_t out_dtype, int64_t probe_column,
                         float* d_probe, void* stream) {
+  return process_device_impl(c, p, d_iq, in_dtype, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, d_cube, d_rd,
+                             out_dtype, probe_column, d_probe, nullptr, stream);
+}
+
+int fmcw_process_slow_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
+                             float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
+                             float* d_slow, void* d_rd, int32_t out_dtype, int32_t* d_frame_list, int64_t* d_len,
+                             float* d_pmax, void* stream) {
+  if (!d_frame_list || !d_len) return fail(FMCW_E_ARG, "d_frame_list / d_len is NULL");
+  if (F == 0 && c) {   // nothing to detect: the leg still starts (L = 0, max(P) = 0)
+    CHK(check_ctx(c, p));
+    hipStream_t s = pick(c, stream);
+    HIPCHK(hipMemsetAsync(d_len, 0, 8, s));
+    if (d_pmax) HIPCHK(hipMemsetAsync(d_pmax, 0, 4, s));
+    return FMCW_OK;
+  }
+  const SlowLeg leg{d_frame_list, d_len, d_pmax};
+  return process_device_impl(c, p, d_iq, in_dtype, F, d_prof, d_count, d_ridx, d_rmag, d_didx, d_slow, nullptr, d_rd,
+                             out_dtype, 0, nullptr, &leg, stream);
+}
+
+static int process_device_impl(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int32_t in_dtype, int64_t F,
+                               float* d_prof, int32_t* d_count, int32_t* d_ridx, float* d_rmag, int32_t* d_didx,
+                               float* d_slow, void* d_cube, void* d_rd, int32_t out_dtype, int64_t probe_column,
+                               float* d_probe, const SlowLeg* leg, void* stream) {
   CHK(check_ctx(c, p));
   if (F < 0) return fail(FMCW_E_ARG, "F < 0");
   if (F == 0) return FMCW_OK;
@@ -910,7 +983,7 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
     }
     if (c->xcd_teams > 0)
       return process_onepass(c, p, d_iq, in_dtype == FMCW_C32H ? 1 : 0, F, d_prof, d_count, d_ridx, d_rmag, d_didx,
-                             d_slow, d_rd, probe_column, d_probe, s);
+                             d_slow, d_rd, probe_column, d_probe, leg, s);
     if (want)
       return fail(FMCW_E_ARG, "XCD schedule: needs 32 CUs per XCD and a grid of one workgroup per CU dealt 32 per XCD");
   }
@@ -1026,6 +1099,10 @@ int fmcw_process_device(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, int
     HIPCHK(hipEventRecord(c->ev_join, sx));
     HIPCHK(hipStreamWaitEvent(s, c->ev_join, 0));
   }
+  if (leg) {   // the streams schedule: the slow-time leg's start as launches of its own
+    HIPCHK(fmcw::launch_compact(d_count, F, C, leg->list, leg->len, s));
+    if (leg->pmax) HIPCHK(hipMemsetAsync(leg->pmax, 0, 4, s));
+  }
   return FMCW_OK;
 }
 
@@ -1121,9 +1198,11 @@ int fmcw_stft_power_device(fmcw_ctx* c, const float* d_slow, const int32_t* d_li
   StageTimer tm(c, 4, s);
   if (fmcw::stft_fast_path(wlen, a.hop)) {        // the reference's 20-tap window: W table + k_stft20
     int st = FMCW_OK;
-    float2* tab = c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
+    bool build = true;
+    float2* tab = fmcw::stft64_form(nfft) ? c->stft_tab64(s, d_win, nfft, &build, &st)
+                                          : c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
     CHK(st);
-    HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
+    if (build) HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
     // device API: d_P is the caller's [max_seg][nfft/2+1] (fmcw.h), the table this stream's
     HIPCHK(fmcw::launch_stft20(a, tab, d_P ? 0 : 1, nullptr, s, max_seg * (int64_t)(nfft / 2 + 1),
                                (int64_t)(nfft / 2 + 1) * 20));
@@ -1158,9 +1237,11 @@ int fmcw_stft_db_direct_device(fmcw_ctx* c, const float* d_slow, const int32_t* 
   a.max_seg = max_seg; a.P = nullptr; a.pmax = const_cast<float*>(d_pmax); a.nseg_out = nullptr;
   StageTimer tm(c, 5, s);
   int st = FMCW_OK;
-  float2* tab = c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
+  bool build = true;
+  float2* tab = fmcw::stft64_form(nfft) ? c->stft_tab64(s, d_win, nfft, &build, &st)
+                                        : c->stft_tab(s, (size_t)(nfft / 2 + 1) * 20 * 8, &st);
   CHK(st);
-  HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
+  if (build) HIPCHK(fmcw::launch_stft_table(d_win, nfft, tab, s));
   HIPCHK(fmcw::launch_stft20(a, tab, 2, d_out, s, max_seg * (int64_t)(nfft / 2 + 1), (int64_t)(nfft / 2 + 1) * 20));
   CHK(c->stft_tab_done(s));
   tm.done();
@@ -1466,8 +1547,11 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       a.inv_fs = (float)(1.0 / fs); a.max_seg = ns; a.bins = reinterpret_cast<int32_t*>(di + o.bins); a.ncol = ncolP;
       StageTimer tm(d, 4, s);
       int st = FMCW_OK;
-      float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table on s
+      float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table buffer on s,
       CHK(st);
+      // rebuilt for this call's window: at nfft 64 the first pass may have kept a cached table
+      // (k_stft64m checks it against the window; this pass's kernel does not)
+      if (fmcw::stft64_form(nf)) HIPCHK(fmcw::launch_stft_table(d_win, nf, tab, s));
       HIPCHK(fmcw::launch_stft20(a, tab, 3, d->s_P.as<float>(), s, (int64_t)(d->s_P.n / 4), (int64_t)(nf / 2 + 1) * 20));
       CHK(d->stft_tab_done(s));
       tm.done();

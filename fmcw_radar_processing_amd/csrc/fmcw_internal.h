@@ -65,7 +65,7 @@ struct DetectParams {
 };
 
 // Single-pass range+Doppler (kernels_xcd.hip, k_rdx): the range cube never
-// reaches HBM; k_detect_1p / k_slow_fix / k_probe (kernels_detect.hip) finish
+// reaches HBM; k_detect_1p / k_probe (kernels_detect.hip) finish
 // the per-frame outputs.
 struct OnePassArgs {
   const void* iq;          // [F][C][S] c64, or c32h when h
@@ -143,21 +143,23 @@ struct Detect1pArgs {
   float* rmag;
   int32_t* didx;
   float* slow_mag;         // [F][C]
-  int32_t* fix_list;       // [F] frames whose slow row must be recomputed
-  int32_t* fix_count;      // device scalar (zeroed by the caller)
-};
-
-struct SlowFixArgs {
+  // the rare target row that was not a group candidate: its slow-time row (:257-259) recomputed
+  // by the frame's own wave, a direct DFT of every chirp at that bin (was the k_slow_fix launch)
   const void* iq;          // [F][C][S] c64, or c32h when h
-  int h;
-  int C, S, NR;
+  int h, S;
   const float4* calw;
   const float2* tw_nr;
-  const int32_t* ridx;     // [F][M]
-  int M;
-  const int32_t* fix_list;
-  const int32_t* fix_count;
-  float* slow_mag;
+  // fused compaction (:257-260, as k_compact), when list != nullptr: every workgroup stores its
+  // counts write-through and adds 1 to *done; the last one scans count_all[0..F_all) (the call's
+  // earlier chunks included), writes list / *len, zeroes *pmax_reset (if set: the running max(P)
+  // of the STFT passes that follow, :276 / :282) and resets *done for the next launch
+  int32_t* done;           // device counter, 0 before the first launch
+  const int32_t* count_all;
+  int64_t F_all;
+  int pn;
+  int32_t* list;
+  int64_t* len;
+  float* pmax_reset;
 };
 
 hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s);
@@ -166,7 +168,6 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s);
 // that is not 32 per XCD, or a grid of one workgroup per CU not dealt 32 per XCD), xcc_team[16]
 // the team index of each HW_REG_XCC_ID.
 hipError_t xcd_census(int* nteams, int8_t* xcc_team);
-hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s);
 
 struct ProbeArgs {          // fft_data column (:410-411) for the single-pass schedule
   const void* iq;          // [F][C][S] of the launch, c64 or c32h (h)
@@ -199,6 +200,8 @@ struct StftArgs {
   int ncol;                // k_stft20 mode 3 / 4: columns in `bins`
   const int32_t* tiles;    // k_stft_mfma mode 1: the 256-segment tiles to cover (device), nullptr = all
   int ntiles;
+  int dbg;                 // diagnostic A/B knob of k_stft64m (FMCW_STFT64_DBG; wrong outputs): 1 no gather,
+                           // 2 no matrix products, 4 no output stores
 };
 
 // 20-tap fast path (kernels_stft.hip k_stft20): W table [nfft/2+1][20] from the window,
@@ -206,6 +209,9 @@ struct StftArgs {
 // a.bins[0..a.ncol) only, written to dst as [seg][ncol], 4 each segment's max of P over the bins
 // a.bins written to dst[seg] (matrix-core form only)
 bool stft_fast_path(int wlen, int hop);
+// the nfft-64 matrix-core kernel (k_stft64m) serves this nfft (not disabled by FMCW_STFT_MFMA=0);
+// it verifies a cached W table against the call's window
+bool stft64_form(int nfft);
 hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_t s);
 // dst_cap: floats available at dst (mode 0: at a.P), tab_cap: float2 entries of tab; a launch
 // whose writes would not fit returns hipErrorInvalidValue before anything is enqueued

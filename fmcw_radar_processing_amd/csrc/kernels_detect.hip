@@ -8,8 +8,9 @@
 //                :227-239 the target row's Doppler peak (read back from RD) with
 //                threshold and fallback, :257-259 the slow-time row |X[ridx, :]|
 //                taken from the group's candidate rows;
-//   k_slow_fix   the rare target row that was not a candidate, recomputed by a
-//                direct DFT of the frame's chirps at that bin;
+//                (the rare target row that was not a candidate: recomputed by the
+//                frame's wave, a direct DFT of its chirps at that bin), and, when
+//                asked, the compaction of :257-260 in its last workgroup;
 //   k_probe      the fft_data column of :410-411 (one chirp), a direct DFT.
 // (ABI 2's 8-tile single pass k_rd1p, which shared these kernels, is retired:
 // the XCD-team schedule reads every frame once instead of 8 times from L2.)
@@ -55,105 +56,177 @@ __global__ __launch_bounds__(1024) void k_probe(ProbeArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// The slow-time row |X[r, k]|, k = 0..C-1, of frame f by a direct DFT at bin r (:203-205 at one
+// bin), one wave: for a target row that was not among its group's candidates (rare: needs a
+// larger non-peak bin of the same group inside the window).
+// ---------------------------------------------------------------------------
+__device__ void slow_row_direct(const Detect1pArgs& a, int64_t f, int r, int lane, float* __restrict__ slow) {
+  const int S = a.S, NR = a.NR, C = a.C;
+  const int nmax = S < NR ? S : NR;
+  for (int k = 0; k < C; ++k) {
+    const int64_t x0 = (f * C + k) * (int64_t)S;
+    auto xc = [&](int n) { return op::ld_iq(a.iq, x0 + n, a.h); };
+    float2 s = make_float2(0.f, 0.f);
+    for (int n = lane; n < S; n += 64) {
+      const float4 c = a.calw[n];
+      s = cadd(s, make_float2(xc(n).x - c.x, xc(n).y - c.y));
+    }
+    s = make_float2(op::wave_sum(s.x), op::wave_sum(s.y));
+    const float2 mu = cscale(s, 1.0f / (float)S);
+    float2 acc = make_float2(0.f, 0.f);
+    for (int n = lane; n < nmax; n += 64) {
+      const float4 c = a.calw[n];
+      const float2 y = cscale(make_float2(xc(n).x - c.x - mu.x, xc(n).y - c.y - mu.y), c.z);
+      const float2 tw = a.tw_nr[((int64_t)n * r) & (NR - 1)];
+      acc = cadd(acc, cmul(y, tw));
+    }
+    acc = make_float2(op::wave_sum(acc.x), op::wave_sum(acc.y));
+    if (lane == 0) slow[k] = sqrtf(cabs2(acc));
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_detect_1p: one wave per frame.  Peak rule on the profile (:211), Doppler
-// index from the row peaks (:227-239), slow-time row from the candidates.
+// index from the row peaks (:227-239), slow-time row from the candidates (or,
+// rarely, by slow_row_direct).  With a.list set, the last workgroup to finish
+// also runs the compaction of :257-260 (what k_compact does) over every frame
+// of the call, so the slow-time leg needs no launch of its own before the STFT.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
   constexpr int NR = op::NR;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t f = (int64_t)blockIdx.x * 4 + w;
-  if (f >= a.nframes) return;
-  const DetectParams& q = a.det;
-  const int C = a.C, M = a.M;
-  int sel[8];
-  float selv[8];
-  const int n = select_peaks<NR, false>(q, lane, a.profile + f * NR, sel, selv);
-  float* slow = a.slow_mag + f * C;
-  if (n > 0) {
-    const int row = sel[0], tt = xcd_group(row);
-    const int32_t* ci = a.cand_idx + (f * a.tiles + tt) * a.ncand;
-    int c = -1;
-    for (int i = a.ncand - 1; i >= 0; --i)
-      if (ci[i] == row) c = i;
-    if (c >= 0) {
-      const float* src = a.cand_rows + ((f * a.tiles + tt) * a.ncand + c) * (int64_t)C;
-      for (int k = lane; k < C; k += 64) slow[k] = sqrtf(src[k]);     // candidates hold |X|^2
-    } else if (lane == 0) {
-      a.fix_list[atomicAdd(a.fix_count, 1)] = (int32_t)f;
+  const bool fused = a.list != nullptr;
+  if (f < a.nframes) {
+    const DetectParams& q = a.det;
+    const int C = a.C, M = a.M;
+    int sel[8];
+    float selv[8];
+    const int n = select_peaks<NR, false>(q, lane, a.profile + f * NR, sel, selv);
+    float* slow = a.slow_mag + f * C;
+    if (n > 0) {
+      const int row = sel[0], tt = xcd_group(row);
+      const int32_t* ci = a.cand_idx + (f * a.tiles + tt) * a.ncand;
+      int c = -1;
+      for (int i = a.ncand - 1; i >= 0; --i)
+        if (ci[i] == row) c = i;
+      if (c >= 0) {
+        const float* src = a.cand_rows + ((f * a.tiles + tt) * a.ncand + c) * (int64_t)C;
+        for (int k = lane; k < C; k += 64) slow[k] = sqrtf(src[k]);     // candidates hold |X|^2
+      } else {
+        slow_row_direct(a, f, row, lane, slow);                         // wave-uniform branch
+      }
+    } else {
+      for (int k = lane; k < C; k += 64) slow[k] = 0.f;
     }
-  } else {
-    for (int k = lane; k < C; k += 64) slow[k] = 0.f;
-  }
-  // :233 [val, di] = max(abs(D)) of each target row: from the RD map when it
-  // was written (k_rd1p then skips the per-row peak search), else from rowpk
-  int2 pkr[8];
-  if (a.rd) {
+    // :233 [val, di] = max(abs(D)) of each target row: from the RD map when it
+    // was written, else from rowpk
+    int2 pkr[8];
+    if (a.rd) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < n) {
-        const int64_t row = (f * NR + sel[j]) * (int64_t)a.ND;
-        float bv = -1.f;
-        int bi = INT_MAX;
-        for (int e = lane; e < a.ND; e += 64) {
-          const float m = sqrtf(cabs2(op::ld_iq(a.rd, row + e, a.rd_h))) * q.rd_unscale;
-          if (m > bv) { bv = m; bi = e; }
+      for (int j = 0; j < 8; ++j)
+        if (j < n) {
+          const int64_t row = (f * NR + sel[j]) * (int64_t)a.ND;
+          float bv = -1.f;
+          int bi = INT_MAX;
+          for (int e = lane; e < a.ND; e += 64) {
+            const float m = sqrtf(cabs2(op::ld_iq(a.rd, row + e, a.rd_h))) * q.rd_unscale;
+            if (m > bv) { bv = m; bi = e; }
+          }
+          wave_argmax(bv, bi);
+          pkr[j] = make_int2(__float_as_int(bv), bi);
         }
-        wave_argmax(bv, bi);
-        pkr[j] = make_int2(__float_as_int(bv), bi);
-      }
-  }
-  if (lane < M) {
-    int ri = 0, di = 0;
-    float rm = 0.f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j == lane && j < n) {
-        const int2 pk = a.rd ? pkr[j] : a.rowpk[f * NR + sel[j]];
-        di = pk.y + 1;
-        if (!(__int_as_float(pk.x) >= q.doppler_thr && di != q.fallback)) di = q.fallback;   // :234-238
-        ri = sel[j] + 1;
-        rm = selv[j];
-      }
-    a.ridx[f * M + lane] = ri;
-    a.rmag[f * M + lane] = rm;
-    a.didx[f * M + lane] = di;
-  }
-  if (lane == 0) a.count[f] = n;
-}
-
-// ---------------------------------------------------------------------------
-// k_slow_fix: |X[ridx, k]| by a direct DFT at one bin, for frames whose target
-// row was not among the tile's candidates (rare: needs a larger non-peak bin
-// of the same tile inside the window).  One wave per chirp.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_slow_fix(SlowFixArgs a) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int nfix = *a.fix_count;
-  const int S = a.S, NR = a.NR, C = a.C;
-  const int nmax = S < NR ? S : NR;
-  for (int i = blockIdx.x; i < nfix; i += gridDim.x) {
-    const int64_t f = a.fix_list[i];
-    const int r = a.ridx[f * a.M] - 1;
-    for (int k = w; k < C; k += 4) {
-      const int64_t x0 = (f * C + k) * (int64_t)S;
-      auto xc = [&](int n) { return op::ld_iq(a.iq, x0 + n, a.h); };
-      float2 s = make_float2(0.f, 0.f);
-      for (int n = lane; n < S; n += 64) {
-        const float4 c = a.calw[n];
-        s = cadd(s, make_float2(xc(n).x - c.x, xc(n).y - c.y));
-      }
-      s = make_float2(op::wave_sum(s.x), op::wave_sum(s.y));
-      const float2 mu = cscale(s, 1.0f / (float)S);
-      float2 acc = make_float2(0.f, 0.f);
-      for (int n = lane; n < nmax; n += 64) {
-        const float4 c = a.calw[n];
-        const float2 y = cscale(make_float2(xc(n).x - c.x - mu.x, xc(n).y - c.y - mu.y), c.z);
-        const float2 tw = a.tw_nr[((int64_t)n * r) & (NR - 1)];
-        acc = cadd(acc, cmul(y, tw));
-      }
-      acc = make_float2(op::wave_sum(acc.x), op::wave_sum(acc.y));
-      if (lane == 0) a.slow_mag[f * C + k] = sqrtf(cabs2(acc));
     }
+    if (lane < M) {
+      int ri = 0, di = 0;
+      float rm = 0.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j == lane && j < n) {
+          const int2 pk = a.rd ? pkr[j] : a.rowpk[f * NR + sel[j]];
+          di = pk.y + 1;
+          if (!(__int_as_float(pk.x) >= q.doppler_thr && di != q.fallback)) di = q.fallback;   // :234-238
+          ri = sel[j] + 1;
+          rm = selv[j];
+        }
+      a.ridx[f * M + lane] = ri;
+      a.rmag[f * M + lane] = rm;
+      a.didx[f * M + lane] = di;
+    }
+    if (lane == 0) {
+      if (fused) __hip_atomic_store(a.count + f, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // write-through (sc1)
+      else a.count[f] = n;
+    }
+  }
+  if (!fused) return;
+  // Hand-off of the counts to the last workgroup (MI355X_MICROARCH.md, inter-workgroup visibility,
+  // the "one lane of each storing workgroup adds to ONE counter" row): sc1 stores, every storing
+  // wave's vmcnt(0), a workgroup barrier, one agent-scope add; the last adder acquires and reads
+  // the counts with sc1 loads.
+  __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // exclusive scan of (count > 0) over F_all frames, 16 consecutive frames per thread per pass
+  __shared__ int wsum[4];
+  int64_t carry = 0;
+  for (int64_t base = 0; base < a.F_all; base += 256 * 16) {
+    const int64_t f0 = base + (int64_t)threadIdx.x * 16;
+    // 16 counts per thread as four 16-byte sc1 buffer loads (all in flight at once)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<int32_t*>(a.count_all), (short)0, (int)(a.F_all * 4 < 0x7fffffff ? a.F_all * 4 : 0x7fffffff), 0x00020000);
+    int4 c4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t fi = f0 + 4 * i;
+      if (fi + 4 <= a.F_all && fi * 4 + 16 <= 0x7fffffffLL) {
+        c4[i] = __builtin_bit_cast(int4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(fi * 4), 0, 16));
+      } else {                                          // the last, partial vector: element by element
+        int e[4];
+        for (int j = 0; j < 4; ++j)
+          e[j] = fi + j < a.F_all ? __hip_atomic_load(a.count_all + fi + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        c4[i] = make_int4(e[0], e[1], e[2], e[3]);
+      }
+    }
+    unsigned bits = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bits |= (c4[i].x > 0 ? 1u : 0u) << (4 * i);
+      bits |= (c4[i].y > 0 ? 1u : 0u) << (4 * i + 1);
+      bits |= (c4[i].z > 0 ? 1u : 0u) << (4 * i + 2);
+      bits |= (c4[i].w > 0 ? 1u : 0u) << (4 * i + 3);
+    }
+    const int mine = __popc(bits);
+    int incl = mine;                                    // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int pre = incl - mine;
+    int tot = 0;
+    for (int i = 0; i < 4; ++i) {
+      if (i < w) pre += wsum[i];
+      tot += wsum[i];
+    }
+    int pos = (int)carry + pre;
+    for (int i = 0; i < 16; ++i)
+      if ((bits >> i) & 1u) a.list[pos++] = (int32_t)(f0 + i);
+    carry += tot;
+    __syncthreads();                                    // wsum reused by the next pass
+  }
+  if (threadIdx.x == 0) {
+    *a.len = carry * a.pn;
+    if (a.pmax_reset) *a.pmax_reset = 0.f;
+    __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -166,11 +239,6 @@ hipError_t launch_detect_1p(const Detect1pArgs& a, hipStream_t s) {
   if (a.nframes <= 0) return hipSuccess;
   if (a.NR != op::NR) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_detect_1p, dim3((unsigned)((a.nframes + 3) / 4)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_slow_fix(const SlowFixArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_slow_fix, dim3(64), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

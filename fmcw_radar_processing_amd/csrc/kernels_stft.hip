@@ -10,6 +10,7 @@
 //   k_synth       SURVEY.md 8d synthetic frames (bench/test input only)
 #include "fft_team.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include "fmcw_internal.h"
 #include "../../include/fmcw.h"
@@ -26,6 +27,15 @@ __device__ __forceinline__ void max_into(float* pmax, float m) {
   unsigned* p = reinterpret_cast<unsigned*>(pmax);
   const unsigned cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (__float_as_uint(m) > cur) atomicMax(p, __float_as_uint(m));
+}
+
+// psd = 20 log10(P / max) (:283) as 20 log10(2) log2(v): the hardware log2 (v_log_f32) and one
+// multiply, 3 instructions against log10f's 13 (which scales denormals and splits log10(2) for an
+// extra-precise product: < 1e-5 dB apart down to -200 dB, against the 1e-3 dB bar of SURVEY 8d).
+// Denormal v (below -759 dB) keeps log10f; v = 0 gives -Inf as MATLAB's G = 0 guard (:551).  Every
+// dB kernel uses it, so the matrix-core and VALU forms stay bit-identical.
+__device__ __forceinline__ float db20(float v) {
+  return v >= 1.17549435e-38f ? 6.0205999132796239f * __log2f(v) : 20.0f * log10f(v);
 }
 
 // ---------------------------------------------------------------------------
@@ -155,15 +165,23 @@ __global__ __launch_bounds__(256) void k_stft_power(StftArgs a, int seg_tile) {
 // ---------------------------------------------------------------------------
 constexpr int STFT_W = 20;
 
+// W[k][m] = w[m] e^{-2 pi i k m / nfft}: exact phase reduction, fp64, rounded once
+__device__ __forceinline__ float2 stft_w(float wm, int k, int m, int nfft) {
+  double sn, cs;
+  sincospi(2.0 * (double)((int64_t)k * m % nfft) / (double)nfft, &sn, &cs);
+  return make_float2((float)(wm * cs), (float)(-wm * sn));
+}
+
+// The table [nfft/2+1][20], followed by the 20 window taps it was built from (the nfft-64 kernel
+// checks them against the window of its call, so a cached table is never used stale)
 __global__ __launch_bounds__(256) void k_stft_table(const float* __restrict__ win, int nfft, float2* __restrict__ tab) {
   const int nb = nfft / 2 + 1;
   const int64_t n = (int64_t)nb * STFT_W;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int k = (int)(i / STFT_W), m = (int)(i - (int64_t)k * STFT_W);
-    double sn, cs;
-    sincospi(2.0 * (double)((int64_t)k * m % nfft) / (double)nfft, &sn, &cs);   // exact phase reduction, fp64
-    tab[i] = make_float2((float)(win[m] * cs), (float)(-win[m] * sn));
+    tab[i] = stft_w(win[m], k, m, nfft);
   }
+  if (blockIdx.x == 0 && threadIdx.x < STFT_W) reinterpret_cast<float*>(tab + n)[threadIdx.x] = win[threadIdx.x];
 }
 
 template <int MODE>
@@ -227,7 +245,7 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
       const float p = fmaf(re, re, im * im) * scale * g;
       if (valid) lmax = fmaxf(lmax, p);
       if constexpr (MODE == 0 || MODE == 3) tile[sl][kk] = p;
-      if constexpr (MODE == 2) tile[sl][kk] = 20.0f * log10f(p * inv);
+      if constexpr (MODE == 2) tile[sl][kk] = db20(p * inv);
     }
     if constexpr (MODE != 1) {
       __syncthreads();
@@ -261,17 +279,22 @@ __global__ __launch_bounds__(256) void k_stft20(StftArgs a, const float2* __rest
 //   bins 16-31.
 // An f32 MFMA is a k-ordered chain of f32 fmas (cdna_hip_programming.md, FP32-input MFMA), so
 // each S(seg, bin) is the same chain over m = 0..19 as k_stft20's v_pk_fma_f32 loop: P, max(P)
-// and the direct dB are bit-identical (tests/test_gpu_stft_mfma.py).  The block's output (256
-// rows of 33 floats, contiguous) goes through LDS and leaves as 16-byte stores.  Lane l of a wave: A = x[seg_base +
+// and the direct dB are bit-identical (tests/test_gpu_stft_mfma.py).  Lane l of a wave: A = x[seg_base +
 // (l & 15) + 4 q + (l >> 4)], B = its tile's W[col = l & 15][m = 4 q + (l >> 4)]; result
-// register r: segment seg_base + 4 (l >> 4) + r, column l & 15.
+// register r: segment seg_base + 4 (l >> 4) + r, column l & 15.  Persistent over 256-segment
+// tiles (round 4: one tile per block, 3,661 blocks whose start-up and two-load gather latency
+// were not covered: 52 us for the max(P) pass, 3x its matrix work); outputs through an LDS tile
+// and whole-line 16-byte stores (4-byte stores straight from the accumulators leave partial
+// lines: 2x slower in the round-5 A/B).
 // ---------------------------------------------------------------------------
 template <int MODE>
 __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __restrict__ tab, float* __restrict__ dst) {
-  constexpr int TS = 256, NB = 33;
+  constexpr int TS = 256, NB = 33, RS = 36, NX = TS * 4 + STFT_W, NPT = (NX + 255) / 256;
   typedef float f4t __attribute__((ext_vector_type(4)));
-  __shared__ float xs[TS * 4 + STFT_W];
-  __shared__ __attribute__((aligned(16))) float tile[MODE == 1 ? 4 : TS * NB];   // the block's [seg][bin] output
+  __shared__ float xs[NX];
+  // the tile of outputs [seg][RS]: 4 RS = 16 (mod 64 banks), so the 4 segment rows of one MFMA
+  // result register (16 columns each) land on disjoint banks (round 4's stride 33: 4-way conflicts)
+  __shared__ __attribute__((aligned(16))) float tile[MODE == 1 ? 4 : TS * RS];
   __shared__ float bmax[4];
   const int64_t L = *a.len;
   const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
@@ -280,29 +303,72 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
   int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / a.hop : 0;   // fix((L-noverlap)/hop)
   if (nseg > a.max_seg) nseg = a.max_seg;
   if (MODE < 2 && blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
-  const int64_t s0 = (int64_t)blockIdx.x * TS;
-  if (s0 >= nseg) return;                                           // block-uniform
-  const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
-  const int nsamp = (ns - 1) * a.hop + STFT_W;
-  const int64_t q0 = s0 * a.hop;
-  for (int i = threadIdx.x; i < TS * a.hop + STFT_W; i += 256) {    // zero past the last segment's samples
-    const int64_t q = q0 + i;
-    xs[i] = i >= nsamp ? 0.f : q < L ? a.slow_mag[(int64_t)a.frame_list[q / a.pn] * a.pn + (q % a.pn)] : a.halo[q - L];
-  }
+  const int64_t ntiles = (nseg + TS - 1) / TS;
+  if ((int64_t)blockIdx.x >= ntiles) return;                        // block-uniform
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
-  // the B operands of the 4 column tiles x 5 k-steps, and sum(w.^2) = sum |W[0][m]|^2
+  const int nx = TS * a.hop + STFT_W;
+  // sample q of the tile starting at q0: q < L is slow_mag[frame_list[q / pn]][q % pn] (one 64-bit
+  // division per tile, uniform; 32-bit ones per sample)
+  const unsigned upn = (unsigned)a.pn;
+  auto gather = [&](int64_t t, float (&v)[NPT]) __attribute__((always_inline)) {
+    if (a.dbg & 1) {
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) v[k] = (float)(threadIdx.x + k);
+      return;
+    }
+    const int64_t s0 = t * TS;
+    const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
+    const int nsamp = (ns - 1) * a.hop + STFT_W;
+    const int64_t q0 = s0 * a.hop;
+    const int64_t fq0 = q0 / a.pn;
+    const unsigned r0 = (unsigned)(q0 - fq0 * a.pn);
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      float x = 0.f;                                                // zero past the last segment's samples
+      if (i < nsamp) {
+        const int64_t q = q0 + i;
+        if (q < L) {
+          const unsigned rr = r0 + (unsigned)i, df = rr / upn;
+          x = a.slow_mag[(int64_t)a.frame_list[fq0 + df] * a.pn + (rr - df * upn)];
+        } else {
+          x = a.halo[q - L];
+        }
+      }
+      v[k] = x;
+    }
+  };
+  float pre[NPT];
+  gather(blockIdx.x, pre);                                          // the first tile's samples in flight
+  // the table may be cached across calls (fmcw_api.cpp stft_tab64): it is used only when the 20
+  // taps stored behind it are this call's window, else every lane forms its W entries itself
+  // (the same fp64 expression as k_stft_table, so the same bits)
+  const float wcall = threadIdx.x < STFT_W ? a.win[threadIdx.x] : 0.f;
+  const float* tabw = reinterpret_cast<const float*>(tab + NB * STFT_W);
+  const bool fresh = __syncthreads_and(threadIdx.x >= STFT_W || tabw[threadIdx.x] == wcall);
+  // the B operands of the 4 column tiles x 5 k-steps (loaded once per block), and sum(w.^2)
   float bw[4][5];
 #pragma unroll
   for (int q = 0; q < 5; ++q) {
     const int m = 4 * q + kq;
-    bw[0][q] = tab[col * STFT_W + m].x;
-    bw[1][q] = col == 0 ? tab[32 * STFT_W + m].x : tab[col * STFT_W + m].y;
-    bw[2][q] = tab[(16 + col) * STFT_W + m].x;
-    bw[3][q] = tab[(16 + col) * STFT_W + m].y;
+    float2 e0, eN, e1;
+    if (fresh) {
+      e0 = tab[col * STFT_W + m]; eN = tab[32 * STFT_W + m]; e1 = tab[(16 + col) * STFT_W + m];
+    } else {
+      const float wm = a.win[m];
+      e0 = stft_w(wm, col, m, 64); eN = stft_w(wm, 32, m, 64); e1 = stft_w(wm, 16 + col, m, 64);
+    }
+    bw[0][q] = e0.x;
+    bw[1][q] = col == 0 ? eN.x : e0.y;
+    bw[2][q] = e1.x;
+    bw[3][q] = e1.y;
   }
   float u = 0.f;
 #pragma unroll
-  for (int m = 0; m < STFT_W; ++m) u = fmaf(tab[m].x, tab[m].x, u);
+  for (int m = 0; m < STFT_W; ++m) {
+    const float wm = fresh ? tab[m].x : a.win[m];                   // W[0][m] = w[m] exactly
+    u = fmaf(wm, wm, u);
+  }
   const float scale = a.inv_fs / u;                                 // 1/(fs*sum(w.^2))
   float inv = 0.f;
   if constexpr (MODE == 2) {
@@ -310,51 +376,81 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
     inv = pm > 0.f ? 1.0f / pm : 0.f;                               // all-zero P: -Inf dB (MATLAB G = 0)
   }
   auto emit = [&](int sl, int b, float p) __attribute__((always_inline)) {
-    if constexpr (MODE == 0) tile[sl * NB + b] = p;
-    if constexpr (MODE == 2) tile[sl * NB + b] = 20.0f * log10f(p * inv);   // :283
+    if constexpr (MODE == 0) tile[sl * RS + b] = p;
+    if constexpr (MODE == 2) tile[sl * RS + b] = db20(p * inv);    // :283
   };
-  __syncthreads();
   float lmax = 0.f;
-#pragma unroll 1
-  for (int g = 0; g < 4; ++g) {                                     // 4 groups of 16 segments per wave
-    const int sb = w * 64 + 16 * g;
-    if (sb >= ns) break;                                            // wave-uniform
-    f4t acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  // Persistent over tiles of 256 segments (grid: a few blocks per CU): the next tile's samples
+  // are loaded while this one is transformed, so the gather's two dependent loads (frame list,
+  // samples) and the block's start-up are paid once per block, not per tile
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t s0 = t * TS;
+    const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
 #pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      const float av = xs[(sb + col) * a.hop + 4 * q + kq];
-#pragma unroll
-      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[t][q], acc[t], 0, 0, 0);
+    for (int k = 0; k < NPT; ++k) {
+      const int i = threadIdx.x + 256 * k;
+      if (i < nx) xs[i] = pre[k];
     }
+    if (t + gridDim.x < ntiles) gather(t + gridDim.x, pre);
+    __syncthreads();                                                // xs holds tile t
+#pragma unroll 1
+    for (int g = 0; g < 4; ++g) {                                   // 4 groups of 16 segments per wave
+      const int sb = w * 64 + 16 * g;
+      if (sb >= ns) break;                                          // wave-uniform
+      f4t acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      if (a.dbg & 2) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int sl = sb + 4 * kq + r;
-      const float re0 = acc[0][r], im0 = col == 0 ? 0.f : acc[1][r];
-      const float p0 = fmaf(re0, re0, im0 * im0) * scale * (col == 0 ? 1.f : 2.f);
-      const float re1 = acc[2][r], im1 = acc[3][r];
-      const float p1 = fmaf(re1, re1, im1 * im1) * scale * 2.f;
-      const float rn = acc[1][r];                                   // column 0: Re S of bin 32
-      const float pn = fmaf(rn, rn, 0.f * 0.f) * scale;
-      if (sl < ns) {
-        if constexpr (MODE < 2) {
-          lmax = fmaxf(lmax, fmaxf(p0, p1));
-          if (col == 0) lmax = fmaxf(lmax, pn);
+        for (int q = 0; q < 5; ++q) {
+          const float av = xs[(sb + col) * a.hop + 4 * q + kq];
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) acc[tt][q & 3] += av * bw[tt][q];
         }
-        emit(sl, col, p0);
-        emit(sl, 16 + col, p1);
-        if (col == 0) emit(sl, 32, pn);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          const float av = xs[(sb + col) * a.hop + 4 * q + kq];
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[tt][q], acc[tt], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int sl = sb + 4 * kq + r;
+        const float re0 = acc[0][r], im0 = col == 0 ? 0.f : acc[1][r];
+        const float p0 = fmaf(re0, re0, im0 * im0) * scale * (col == 0 ? 1.f : 2.f);
+        const float re1 = acc[2][r], im1 = acc[3][r];
+        const float p1 = fmaf(re1, re1, im1 * im1) * scale * 2.f;
+        const float rn = acc[1][r];                                 // column 0: Re S of bin 32
+        const float pn = fmaf(rn, rn, 0.f * 0.f) * scale;
+        if (sl < ns) {
+          if constexpr (MODE < 2) {
+            lmax = fmaxf(lmax, fmaxf(p0, p1));
+            if (col == 0) lmax = fmaxf(lmax, pn);
+          }
+          emit(sl, col, p0);
+          emit(sl, 16 + col, p1);
+          if (col == 0) emit(sl, 32, pn);
+        }
       }
     }
-  }
-  if constexpr (MODE != 1) {
-    // the block's rows s0 .. s0+ns-1 are one contiguous run of ns x 33 floats, 16-byte aligned
-    // (s0 x 33 x 4 = 33792 b): coalesced 16-byte stores
-    __syncthreads();
-    float* out = (MODE == 0 ? a.P : dst) + s0 * NB;
-    const int n = ns * NB, n4 = n >> 2;
-    const f4t* t4 = reinterpret_cast<const f4t*>(tile);
-    for (int i = threadIdx.x; i < n4; i += 256) reinterpret_cast<f4t*>(out)[i] = t4[i];
-    for (int i = 4 * n4 + threadIdx.x; i < n; i += 256) out[i] = tile[i];
+    __syncthreads();                                                // xs read out; the tile written
+    if (MODE != 1 && !(a.dbg & 4)) {
+      // the tile's rows s0 .. s0+ns-1 are one contiguous run of ns x 33 floats, 16-byte aligned
+      // (s0 x 33 x 4 = 33792 t bytes): whole-line 16-byte stores
+      float* out = (MODE == 0 ? a.P : dst) + s0 * NB;
+      const int n = ns * NB, n4 = n >> 2;
+      for (int i = threadIdx.x; i < n4; i += 256) {
+        f4t v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int o = 4 * i + e, rr = o / NB;
+          v[e] = tile[rr * RS + (o - rr * NB)];
+        }
+        reinterpret_cast<f4t*>(out)[i] = v;
+      }
+      for (int o = 4 * n4 + threadIdx.x; o < n; o += 256) out[o] = tile[(o / NB) * RS + o % NB];
+      __syncthreads();                                              // the tile read out
+    }
   }
   if constexpr (MODE < 2) {
 #pragma unroll
@@ -467,8 +563,8 @@ __global__ __launch_bounds__(256) void k_stft_mfma(StftArgs a, const float2* __r
           tile[sl * (KC + 1) + 16 + col] = p1;
         }
         if constexpr (MODE == 2) {
-          tile[sl * (KC + 1) + col] = 20.0f * log10f(p0 * inv);
-          tile[sl * (KC + 1) + 16 + col] = 20.0f * log10f(p1 * inv);
+          tile[sl * (KC + 1) + col] = db20(p0 * inv);
+          tile[sl * (KC + 1) + 16 + col] = db20(p1 * inv);
         }
       }
     }
@@ -510,11 +606,11 @@ __global__ __launch_bounds__(256) void k_stft_db(StftDbArgs a) {
     const int j = (int)(o - s * nout);
     const float* row = a.P + s * a.nbins_in;
     if (a.nlog == 0) {
-      a.out[o] = 20.0f * log10f(row[j] * inv);                     // :283
+      a.out[o] = db20(row[j] * inv);                                // :283
     } else {
       const int i0 = a.lidx[j];
       const float w = a.lw[j];
-      const float d0 = 20.0f * log10f(row[i0] * inv), d1 = 20.0f * log10f(row[i0 + 1] * inv);
+      const float d0 = db20(row[i0] * inv), d1 = db20(row[i0 + 1] * inv);
       a.out[o] = d0 + w * (d1 - d0);                               // :299 interp1 'linear','extrap'
     }
   }
@@ -533,11 +629,10 @@ __global__ __launch_bounds__(256) void k_stft_db_flat(StftDbArgs a) {
   f4t* out = reinterpret_cast<f4t*>(a.out);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const f4t v = in[i];
-    out[i] = f4t{20.0f * log10f(v.x * inv), 20.0f * log10f(v.y * inv), 20.0f * log10f(v.z * inv),
-                 20.0f * log10f(v.w * inv)};
+    out[i] = f4t{db20(v.x * inv), db20(v.y * inv), db20(v.z * inv), db20(v.w * inv)};
   }
   for (int64_t i = 4 * n4 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    a.out[i] = 20.0f * log10f(a.P[i] * inv);
+    a.out[i] = db20(a.P[i] * inv);
 }
 
 // ---------------------------------------------------------------------------
@@ -622,6 +717,11 @@ hipError_t launch_compact(const int32_t* count, int64_t F, int pn, int32_t* list
 
 bool stft_fast_path(int wlen, int hop) { return wlen == STFT_W && hop >= 1 && hop <= 4; }
 
+bool stft64_form(int nfft) {
+  const char* mf = std::getenv("FMCW_STFT_MFMA");
+  return nfft == 64 && !(mf && mf[0] == '0');
+}
+
 hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_t s) {
   const int64_t n = (int64_t)(nfft / 2 + 1) * STFT_W;
   hipLaunchKernelGGL(k_stft_table, dim3(grid_for(n)), dim3(256), 0, s, win, nfft, tab);
@@ -656,12 +756,25 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
   const dim3 grid((unsigned)blocks, (unsigned)((ncol + col_chunk - 1) / col_chunk));
   // nfft 64 (config 4): P / max(P) on the matrix cores, bit-identical (FMCW_STFT_MFMA=0: VALU)
   const char* mf = std::getenv("FMCW_STFT_MFMA");
-  const float* outp = mode == 0 ? a.P : dst;
   if ((mode == 4 || a.tiles) && mf && mf[0] == '0') return hipErrorInvalidValue;   // matrix-core form only
-  if (a.nfft == 64 && mode <= 2 && !a.tiles && !(mf && mf[0] == '0') && (mode == 1 || (reinterpret_cast<uintptr_t>(outp) & 15) == 0)) {
-    if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
-    else if (mode == 1) hipLaunchKernelGGL(k_stft64m<1>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
-    else hipLaunchKernelGGL(k_stft64m<2>, dim3((unsigned)blocks), dim3(256), 0, s, a, tab, dst);
+  if (stft64_form(a.nfft) && mode <= 2 && !a.tiles) {
+    // persistent: a few blocks per CU loop over the tiles (nseg is on the device: the grid covers
+    // max_seg's tiles at most, the blocks past the last tile return)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    }
+    int bpc = 3;
+    if (const char* e = std::getenv("FMCW_STFT64_BPC")) bpc = std::max(1, std::min(16, std::atoi(e)));   // A/B
+    const unsigned g = (unsigned)std::min<int64_t>(blocks, (int64_t)cus * bpc);
+    StftArgs ad = a;
+    if (const char* e = std::getenv("FMCW_STFT64_DBG")) ad.dbg = std::atoi(e);   // diagnostics only
+    const StftArgs& a = ad;
+    if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3(g), dim3(256), 0, s, a, tab, dst);
+    else if (mode == 1) hipLaunchKernelGGL(k_stft64m<1>, dim3(g), dim3(256), 0, s, a, tab, dst);
+    else hipLaunchKernelGGL(k_stft64m<2>, dim3(g), dim3(256), 0, s, a, tab, dst);
     return hipGetLastError();
   }
   if (!(mf && mf[0] == '0')) {      // any other nfft: 32-bin column chunks on the matrix cores

@@ -186,6 +186,18 @@ class Engine:
                 _ptr(outs["tgt_doppler_idx"]), _ptr(outs["slow_mag"]), _ptr(d_cube), _ptr(d_rd), out_dtype,
                 int(probe_column), _ptr(outs.get("probe_mag")), hs))
 
+    def process_slow_device(self, d_iq, F: int, in_dtype: int, outs: dict, d_list, d_len, d_pmax=None, d_rd=None,
+                            out_dtype: int = FMCW_C64, stream=None) -> None:
+        """process_device + compact_device (+ d_pmax = 0) in one call (fmcw_process_slow_device): on
+        the single-pass schedule the compaction runs in the detection kernel's last workgroup."""
+        self._need()
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_process_slow_device(
+                self.h, ct.byref(self.p), _ptr(d_iq), in_dtype, int(F), _ptr(outs["profile"]),
+                _ptr(outs["tgt_count"]), _ptr(outs["tgt_range_idx"]), _ptr(outs["tgt_range_mag"]),
+                _ptr(outs["tgt_doppler_idx"]), _ptr(outs["slow_mag"]), _ptr(d_rd), out_dtype, _ptr(d_list),
+                _ptr(d_len), _ptr(d_pmax), hs))
+
     def range_fft_device(self, d_iq, F: int, in_dtype: int, d_cube, d_prof, out_dtype: int = FMCW_C64,
                          stream=None) -> None:
         self._need()

@@ -40,7 +40,7 @@ extern "C" {
 
 /* 3: FMCW_PIPE_ONEPASS names the XCD-team schedule (E_ARG where the XCD census fails),
  *    fmcw_default_devices, FMCW_JSON_BOOL */
-#define FMCW_ABI_VERSION 3
+#define FMCW_ABI_VERSION 4
 
 typedef enum fmcw_status {
   FMCW_OK = 0,
@@ -190,6 +190,20 @@ int fmcw_process_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, i
 int fmcw_range_fft_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, int32_t in_dtype,
                           int64_t F, void* d_range_cube, int32_t out_dtype, float* d_range_profile,
                           void* stream);
+
+/* fmcw_process_device (no range cube, no probe column) followed by the start of the slow-time
+ * leg, in one call (ABI 4): the compaction of :257-260 -- d_frame_list / *d_len exactly as
+ * fmcw_compact_device(d_tgt_count, F, pn, ...) -- and *d_pmax = 0 (when d_pmax != NULL) for the
+ * STFT passes that follow (fmcw_stft_power_device's running max(P), :276 / :282).  On the
+ * single-pass schedule both run inside the detection kernel (its last workgroup), so the leg
+ * costs no launches of its own (the reference's :257-260 append and the spectrogram call
+ * `radar_processing.m:259`, `:276`). */
+int fmcw_process_slow_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, int32_t in_dtype,
+                             int64_t F, float* d_range_profile, int32_t* d_tgt_count,
+                             int32_t* d_tgt_range_idx, float* d_tgt_range_mag,
+                             int32_t* d_tgt_doppler_idx, float* d_slow_mag, void* d_rd_map,
+                             int32_t out_dtype, int32_t* d_frame_list, int64_t* d_len, float* d_pmax,
+                             void* stream);
 
 /* Slow-time compaction (:257-260): exclusive scan of (tgt_count>0) over F
  * frames.  Writes d_frame_list[i] = i-th frame with a target, *d_len = L

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_error_string():
     lib = _lib.load()
-    assert lib.fmcw_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.fmcw_abi_version() == _lib.ABI_VERSION == 4
     assert isinstance(lib.fmcw_last_error(), bytes)
 
 

@@ -56,6 +56,24 @@ def test_gpus_2_names_config5_and_the_frame_total():
     assert bench.config_block(8, 4096, 2)["covers_config5_stream"]
 
 
+@pytest.mark.parametrize("args", [["--gpus", "2", "--stream-frames", "65536"],
+                                  ["--gpus", "3", "--frames", "512", "--steps", "2"]])
+def test_dry_dist_runs_the_step_exchange(args):
+    """the ranks run exactly the step's collective sequence (bench.exchange_halo
+    -> the STFT leg's max(P) all_reduce -> bench.exchange_rows) on CPU tensors of the step's
+    shapes, every step of the run (65,536 frames over 2 ranks: 8 steps of 4096 frames; 3 ranks
+    with an empty slow-time shard in the middle at step 0), and each rank checks what it received
+    (halo, lengths, max, the range_speed rows on rank 0)."""
+    r = _run_bench(args + ["--dry-dist"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    ex = d["exchange"]
+    assert ex["all_ranks_ok"] and ex["halo"] and ex["lengths"] and ex["max"] and ex["rows"], ex
+    assert ex["steps"] == d["steps"] and d["n_gpus"] == int(args[1])
+    if "--stream-frames" in args:
+        assert d["config"]["covers_config5_stream"] and d["steps"] == 8
+
+
 def test_stream_frames_must_divide():
     r = _run_bench(["--gpus", "2", "--dry-dist", "--stream-frames", "65537"])
     assert r.returncode == 2 and "not a multiple" in r.stderr
