@@ -65,6 +65,8 @@ def parse():
                     help="dB of the STFT leg: stored = pass 1 writes P and max(P), pass 2 turns P into dB in "
                          "place (0.103 ms per step); direct = pass 1 max(P) only, pass 2 recomputes P and writes "
                          "dB, P never stored (0.124 ms; profiles/r04g_stft_ab.txt)")
+    ap.add_argument("--no-copy-ceiling", action="store_true",
+                    help="skip the in-run HBM copy ceiling of k_rdx's bytes (roofline.copy_ceiling_ms)")
     ap.add_argument("--dry-dist", action="store_true",
                     help="launcher test without a GPU: the ranks meet over gloo and rank 0 prints n_gpus")
     return ap.parse_args()
@@ -293,6 +295,30 @@ def main():
     # sanity: the step did real work (detections on most frames)
     det = int((outs["tgt_count"] > 0).sum().item())
 
+    # ---- in-run normalisers of the roofline --------------------------
+    # the effective shader clock of the last k_rdx launch (in-kernel stamps) and the HBM copy
+    # ceiling of k_rdx's bytes in this process on this box: a 16-byte nontemporal copy of the input
+    # cube into an RD-sized buffer (8.6 + 8.6 GB, DESIGN 4.0.1 part A's shape)
+    sclk_mhz, _ = eng.rdx_clock()
+    copy = None
+    if not args.no_copy_ceiling:
+        nbytes = d_iq.numel() * d_iq.element_size()
+        d_cp = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+        eng.copy_device(d_iq, d_cp, nbytes, stream=stream)
+        torch.cuda.synchronize(dev)
+        reps = 5
+        ca, cb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ca.record(stream)
+        for _ in range(reps):
+            eng.copy_device(d_iq, d_cp, nbytes, stream=stream)
+        cb.record(stream)
+        torch.cuda.synchronize(dev)
+        cms = ca.elapsed_time(cb) / reps
+        del d_cp
+        copy = {"ms": round(cms, 4), "bytes": 2 * nbytes, "GBps": round(2 * nbytes / (cms * 1e-3) / 1e9, 1),
+                "what": "16-byte nontemporal copy of the input cube into an RD-sized buffer (k_rdx's in + RD bytes), "
+                        "one thread per 16 bytes, HIP events, same process"}
+
     # ---- roofline ----------------------------------------------------------------
     # path: SURVEY.md 8d config-4 algorithmic bytes per frame (input + RD map +
     # profile + slow-time row; the range cube is an intermediate) over the
@@ -340,6 +366,13 @@ def main():
                 "alg_bytes_per_launch": k["alg_bytes_per_launch"], "avg_launch_us": k["avg_launch_us"],
                 "frames_per_launch": k["frames_per_launch"],
                 "traffic_source": pmc.get("source") if pmc and traffic else None}
+        if dom == "k_rdx":
+            roof["sclk_mhz"] = round(sclk_mhz, 1) if sclk_mhz else None
+            if copy:
+                copy_ms_launch = copy["ms"] * (k["alg_bytes_per_launch"] / copy["bytes"])
+                roof["copy_ceiling_ms"] = round(copy_ms_launch, 4)
+                roof["frac_of_copy_ceiling"] = round(copy_ms_launch / (k["avg_launch_us"] * 1e-3), 4)
+                roof["copy_ceiling"] = copy
 
     # ---- input fan-out over xGMI from rank 0 (reported separately, not in value) -----
     fanout = None

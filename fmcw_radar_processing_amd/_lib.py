@@ -84,6 +84,8 @@ SIGNATURES = {
     "fmcw_set_chunk_frames": (ct.c_int, [_P, _I64]),
     "fmcw_set_pipeline": (ct.c_int, [_P, _I32]),
     "fmcw_synchronize": (ct.c_int, [_P]),
+    "fmcw_rdx_clock": (ct.c_int, [_P, ct.POINTER(_D), ct.POINTER(_D)]),
+    "fmcw_copy_device": (ct.c_int, [_P, _P, _P, _I64, _P]),
     "fmcw_json_write": (ct.c_int, [ct.c_char_p, ct.POINTER(JsonField), _I32, _I32, _I32, ct.POINTER(_I64)]),
     "fmcw_stft_png": (ct.c_int, [_P, _P, _I64, _P, _I32, _I32, _I32, _D, _I32, _P, _P, _P, ct.c_char_p, _I32, _I32,
                                  ct.POINTER(_I64)]),

@@ -317,6 +317,7 @@ struct fmcw_ctx {
   int pipe_mode = FMCW_PIPE_AUTO;
   DevBuf op_rowpk, op_cidx, op_crows;           // single-pass schedule scratch (per chunk)
   DevBuf x_cube, x_ctr, x_err, x_tab;          // XCD-team schedule: hand-off slots, counters, sticky error, XT_* table
+  DevBuf x_clk;                                // k_rdx's clock stamps of its last launch (fmcw_rdx_clock)
   int xcd_teams = -1;                          // census of the device: its XCD teams (-1 not run yet, 0 none)
   int8_t xcc_team[16] = {};                    // HW_REG_XCC_ID -> team
   bool xcd_used = false;                       // a k_rdx launch since the last error check
@@ -685,6 +686,31 @@ static int xcd_check(fmcw_ctx* c) {
                                   : "XCD schedule: a range-cube hand-off timed out (outputs invalid)");
 }
 
+int fmcw_rdx_clock(fmcw_ctx* c, double* mhz, double* us) {
+  if (!c || !mhz) return fail(FMCW_E_ARG, "ctx / mhz is NULL");
+  *mhz = 0.0;
+  if (us) *us = 0.0;
+  CHK(set_device(c));
+  if (!c->x_clk.p) return FMCW_OK;             // no k_rdx launch yet
+  unsigned long long h[4] = {};
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpy(h, c->x_clk.p, sizeof(h), hipMemcpyDeviceToHost));
+  if (h[3] > h[1] && h[2] > h[0]) {
+    *mhz = (double)(h[2] - h[0]) / (double)(h[3] - h[1]) * 100.0;   // s_memrealtime: 100 MHz
+    if (us) *us = (double)(h[3] - h[1]) / 100.0;
+  }
+  return FMCW_OK;
+}
+
+int fmcw_copy_device(fmcw_ctx* c, const void* d_src, void* d_dst, int64_t bytes, void* stream) {
+  if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
+  if (!d_src || !d_dst || bytes < 0) return fail(FMCW_E_ARG, "bad copy arguments");
+  CHK(set_device(c));
+  HIPCHK(fmcw::launch_copy16(d_src, d_dst, bytes, pick(c, stream)));
+  return FMCW_OK;
+}
+
 int fmcw_synchronize(fmcw_ctx* c) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
   CHK(set_device(c));
@@ -805,6 +831,10 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   {
     CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8));
     CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
+    if (!c->x_clk.p) {
+      CHK(c->x_clk.ensure(4 * sizeof(unsigned long long)));
+      HIPCHK(hipMemsetAsync(c->x_clk.p, 0, 4 * sizeof(unsigned long long), s));
+    }
     if (!c->x_err.p) {
       CHK(c->x_err.ensure(sizeof(unsigned)));
       HIPCHK(hipMemsetAsync(c->x_err.p, 0, sizeof(unsigned), s));
@@ -849,6 +879,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
     a.xcube = c->x_cube.as<float2>(); a.xctr = c->x_ctr.as<unsigned>(); a.xerr = c->x_err.as<unsigned>();
     a.slots = slots; a.xtab = c->x_tab.as<float2>(); a.cal_sum = c->cal_sum;
+    a.clk = c->x_clk.as<unsigned long long>();
     a.s16mask = h ? host_s16mask(p, NR) : 0u;
     a.nteams = c->xcd_teams > 0 ? c->xcd_teams : 0;
     std::memcpy(a.xcc_team, c->xcc_team, sizeof(a.xcc_team));

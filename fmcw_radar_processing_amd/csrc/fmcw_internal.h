@@ -86,6 +86,8 @@ struct OnePassArgs {
   int force_fix;           // test knob (FMCW_ONEPASS_FORCE_FIX=1): keep no candidates, so every
                            // slow-time row goes through k_slow_fix
   unsigned long long* dbg; // diagnostic builds only (-DXK_STAMPS): [blocks][8] s_memrealtime stamps
+  unsigned long long* clk; // or nullptr: {shader clock, 100 MHz clock} at the start and the end of team 0's
+                           // member 0 (k_rdx's effective clock, fmcw_rdx_clock)
   // XCD-team schedule (k_rdx) only:
   float2* xcube;           // [8 XCDs][slots][XCD_TILES groups][C][32] range-cube hand-off slots
   unsigned* xctr;          // [8 XCDs][2: ready, (unused)][XCD_MAX_SLOTS][32] + [8][32] tickets + the abort word:
@@ -250,6 +252,8 @@ hipError_t launch_stft_power(const StftArgs& a, hipStream_t s);
 hipError_t launch_stft_db(const StftDbArgs& a, hipStream_t s);
 hipError_t launch_synth(const SynthArgs& a, hipStream_t s);
 hipError_t launch_fill_u32(uint32_t* p, uint32_t v, int64_t n, hipStream_t s);
+// kernels_util.hip: the bench's HBM copy ceiling (16-byte nontemporal loads and stores)
+hipError_t launch_copy16(const void* src, void* dst, int64_t bytes, hipStream_t s);
 
 
 bool range_size_supported(int nr);

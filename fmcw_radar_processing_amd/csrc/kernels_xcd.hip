@@ -217,6 +217,12 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   __syncthreads();
   const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
   if (k >= NK) return;                 // more than 32 blocks on one XCD: its team is short (waits time out)
+  // the effective shader clock of the launch: team 0's member 0 stamps both clocks (vector stores)
+  const bool stamper = a.clk != nullptr && x == 0 && k == 0 && tid == 0;
+  if (stamper) {
+    a.clk[0] = __builtin_amdgcn_s_memtime();
+    a.clk[1] = __builtin_amdgcn_s_memrealtime();
+  }
   const int T = a.nteams;              // teams (XCDs) of the device: frames x + T j for team x
   const int nj = a.F > x ? (int)((a.F - x + T - 1) / T) : 0;
   const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
@@ -539,6 +545,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       xv[4 * g + 2] = (xv[4 * g + 2] - mu) * wv.z;
       xv[4 * g + 3] = (xv[4 * g + 3] - mu) * wv.w;
     }
+#ifndef XK_NODOPFFT   // diagnostic A/B (wrong outputs): the Doppler DFTs, twiddles and transpose removed
     dft16p<1>(xv);
 #pragma unroll
     for (int d0 = 1; d0 < 16; d0 += 2) {
@@ -546,6 +553,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       xv[d0] = cmul_a(xv[d0], t.xy);
       if (d0 < 15) xv[d0 + 1] = cmul_a(xv[d0 + 1], t.zw);
     }
+#endif
   };
   auto d_td = [&](c2 (&xv)[16]) __attribute__((always_inline)) {
 #pragma unroll
@@ -672,14 +680,18 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       ld_group(slot(j - kLag) + (int64_t)k * C * GP * kES, grp, G16);
     }
     stamp(7);
+#ifndef XK_NODOPFFT
     if (dj) d_td(xv);
+#endif
     if (rj) {
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
         *reinterpret_cast<f4v*>(&rt[kk * 136 + 2 * lane]) = f4v{z0[kk].x, z0[kk].y, z1[kk].x, z1[kk].y};
       cfence();
     }
+#ifndef XK_NODOPFFT
     if (dj) dft16p<1>(xv);             // lane (pp, d0 = q): D[q + 16 d1] = xv[d1]
+#endif
     if (rj) {
 #pragma unroll
       for (int a1 = 0; a1 < 16; ++a1) u[a1] = rt[k1 * 136 + a0 + 8 * a1];
@@ -754,6 +766,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     else run(F_{});
   } else {
     run(F_{});
+  }
+  if (stamper) {
+    a.clk[2] = __builtin_amdgcn_s_memtime();
+    a.clk[3] = __builtin_amdgcn_s_memrealtime();
   }
 #ifdef XK_STAMPS
   if (lane == 0 && (w == 0 || w == 4)) {

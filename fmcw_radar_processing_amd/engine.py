@@ -261,6 +261,17 @@ class Engine:
     def synchronize(self) -> None:
         check(self.lib.fmcw_synchronize(self.h))
 
+    def rdx_clock(self) -> tuple:
+        """(MHz, us) of the last k_rdx launch: its effective shader clock and stamped span."""
+        mhz, us = ct.c_double(), ct.c_double()
+        check(self.lib.fmcw_rdx_clock(self.h, ct.byref(mhz), ct.byref(us)))
+        return mhz.value, us.value
+
+    def copy_device(self, d_src, d_dst, nbytes: int, stream=None) -> None:
+        """16-byte nontemporal device copy (the bench's HBM copy ceiling)."""
+        with _sided(stream) as hs:
+            check(self.lib.fmcw_copy_device(self.h, _ptr(d_src), _ptr(d_dst), int(nbytes), hs))
+
     def _need(self) -> FmcwConfig:
         if self.cfg is None:
             raise FmcwError(_lib.FMCW_E_STATE, "set_taps() first")

@@ -294,6 +294,15 @@ int fmcw_set_pipeline(fmcw_ctx* ctx, int32_t mode);
 
 int fmcw_synchronize(fmcw_ctx* ctx);
 
+/* Measurement helpers of the bench line (ABI 4; no part of the reference's path).
+ * fmcw_rdx_clock: the effective shader clock (MHz) of the context's last k_rdx launch, from the
+ *   shader-clock and 100 MHz stamps one member takes at its start and its end (*us: that span);
+ *   0 when no launch ran.  Synchronises the device.
+ * fmcw_copy_device: a 16-byte nontemporal copy of `bytes` (a multiple of 16, 16-byte aligned
+ *   pointers), asynchronous on `stream`: the HBM copy ceiling of k_rdx's bytes (bench.py). */
+int fmcw_rdx_clock(fmcw_ctx* ctx, double* mhz, double* us);
+int fmcw_copy_device(fmcw_ctx* ctx, const void* d_src, void* d_dst, int64_t bytes, void* stream);
+
 /* ---------------------------------------------------------------------------
  * spectrogram.png, replacing radar_processing.m:331-348:
  *   surf(T, fftshift(F), fftshift(psd,1), 'EdgeColor','none'); view(0,90);
