@@ -271,9 +271,10 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     sticky_check(eng, "warmup")
-    # level 2: HIP events around every K1/K2/K3 launch on its own stream (the
-    # per-kernel roofline below) plus the range+Doppler span and STFT launches
-    level = 0 if args.no_stage_timing else 2
+    # level 3: HIP events around every launch of the dominant kernel only (k_rdx; the roofline
+    # below), on its stream -- each event pair costs the step a few microseconds (round 5: level 2,
+    # a pair around every stage, took 43 us of a 4.6-ms step)
+    level = 0 if args.no_stage_timing else 3
     eng.timing(level)
     eng.timing_reset()
     barrier()
@@ -287,6 +288,18 @@ def main():
     stages = eng.timing_read() if level else {}
     eng.timing(0)
     sticky_check(eng, "timed steps")          # a timed-out k_rdx hand-off invalidates the run
+    # the stage breakdown (every launch between event pairs) from a few steps after the timed ones
+    breakdown = {}
+    if level:
+        eng.timing(2)
+        eng.timing_reset()
+        nb_steps = 5
+        for _ in range(nb_steps):
+            step()
+        torch.cuda.synchronize(dev)
+        breakdown = {k: (ms / nb_steps, n) for k, (ms, n) in eng.timing_read().items()}
+        eng.timing(0)
+        sticky_check(eng, "stage breakdown steps")
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -334,8 +347,12 @@ def main():
                                    ("onepass", "k_rdx", C * S * esz + NR * ND * esz + NR * 4),
                                    ("detect", "k_detect", None)):
         ms, n = stages.get(name, (0.0, 0))
+        steps_of = args.steps
+        if not n and name in breakdown:            # stages the timed region does not time (level 3)
+            ms, n = breakdown[name]
+            ms, steps_of = ms * 5, 5
         if n:
-            fpl = F * args.steps / n
+            fpl = F * steps_of / n
             us = ms / n * 1e3
             kern[label] = {"avg_launch_us": round(us, 2), "frames_per_launch": fpl}
             if per_frame:
@@ -343,9 +360,13 @@ def main():
                 kern[label]["achieved_GBps"] = round(per_frame * fpl / (us * 1e-6) / 1e9, 1)
     roof, path = None, None
     rd_ms, rd_n = stages.get("range_doppler", (0.0, 0))
+    rd_steps = args.steps
+    if not rd_n and "range_doppler" in breakdown:
+        rd_ms, rd_n = breakdown["range_doppler"]
+        rd_ms, rd_steps = rd_ms * 5, 5
     if rd_n:
         per_launch_ms = rd_ms / rd_n
-        fpl = F * args.steps / rd_n
+        fpl = F * rd_steps / rd_n
         ach = alg_per_frame * fpl / (per_launch_ms * 1e-3) / 1e9
         path = {"achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBPS, 4), "unit": "GB/s",
                 "span_us": round(per_launch_ms * 1e3, 2), "frames_per_span": fpl, "alg_bytes_per_frame": alg_per_frame,
@@ -428,7 +449,9 @@ def main():
             "kernels": kern,
             "cpu_baseline": cpu,
             "checked": checked,
-            "stages_ms_per_step": {k: round(v[0] / args.steps, 4) for k, v in stages.items() if v[1]},
+            "stages_ms_per_step": {k: round(v[0], 4) for k, v in breakdown.items() if v[1]},
+            "stages_note": "HIP-event pairs around every launch, 5 steps after the timed ones (the timed steps carry "
+                           "k_rdx's pair only)",
             "frames_with_target": det,
         }
         if fanout:
@@ -569,7 +592,7 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
         step()
     torch.cuda.synchronize(dev)
     sticky_check(eng, "fp16 warmup")
-    eng.timing(2)
+    eng.timing(3)
     eng.timing_reset()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -613,7 +636,7 @@ def bench_config2(eng, args, dev, stream, pmc):
     for _ in range(warm2):
         eng.range_fft_device(d_iq, F2, FMCW_C64, d_cube, d_prof, stream=stream)
     torch.cuda.synchronize(dev)
-    eng.timing(1)
+    eng.timing(3)
     eng.timing_reset()
     t0 = time.perf_counter()
     for _ in range(reps2):

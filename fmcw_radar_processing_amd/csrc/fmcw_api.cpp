@@ -378,7 +378,10 @@ struct StageTimer {
   hipStream_t s;
   hipEvent_t a = nullptr;
   StageTimer(fmcw_ctx* c_, int st, hipStream_t s_, int level = 1) : c(c_), stage(st), s(s_) {
-    if (c->timing >= level) {
+    // level 3: only the dominant kernels' launches (k_rdx, stage 8; K1 range-only, stage 6):
+    // every event pair on the stream costs the step a few microseconds
+    const bool on = c->timing == 3 ? (st == 6 || st == 8) : c->timing >= level;
+    if (on) {
       a = c->get_event();
       if (a) (void)hipEventRecord(a, s);
     }
@@ -720,7 +723,7 @@ int fmcw_synchronize(fmcw_ctx* c) {
 
 int fmcw_timing_enable(fmcw_ctx* c, int32_t enable) {
   if (!c) return fail(FMCW_E_ARG, "ctx is NULL");
-  if (enable < 0 || enable > 2) return fail(FMCW_E_ARG, "timing level must be 0, 1 or 2");
+  if (enable < 0 || enable > 3) return fail(FMCW_E_ARG, "timing level must be 0, 1, 2 or 3");
   c->timing = enable;
   return FMCW_OK;   // device 0 only: the timers are the device-pointer calls' (benches)
 }

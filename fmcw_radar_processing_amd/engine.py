@@ -244,7 +244,8 @@ class Engine:
 
     # ---- timing -----------------------------------------------------------------
     def timing(self, level: int) -> None:
-        """0 off, 1 per range+Doppler chunk + STFT launches, 2 per kernel launch."""
+        """0 off, 1 per range+Doppler chunk + STFT launches, 2 per kernel launch, 3 the dominant
+        kernel's launches only (k_rdx / range-only K1)."""
         check(self.lib.fmcw_timing_enable(self.h, int(level)))
 
     def timing_reset(self) -> None:

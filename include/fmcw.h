@@ -254,7 +254,9 @@ int fmcw_synth_device(fmcw_ctx* ctx, const fmcw_params* p, int64_t frame0, int64
  * enable: 0 off; 1 = the range+Doppler span of each fmcw_process_device call
  * (stage 7: event before the first range launch .. event after the last
  * Doppler launch; the chunks run as a 3-stream software pipeline) and one pair
- * per STFT-side launch (stages 3-6); 2 = additionally one pair per K1/K2/K3.
+ * per STFT-side launch (stages 3-6); 2 = additionally one pair per K1/K2/K3; 3 = only the
+ * dominant kernel's launches (stage 8 k_rdx, stage 6 range-only K1), the cheapest form for a
+ * timed run (each event pair costs the stream a few microseconds).
  * stage: 0 range, 1 doppler, 2 detect, 3 compact, 4 stft_power, 5 stft_db,
  *        6 range_only, 7 range+Doppler span, 8 k_rdx (single-pass schedule,
  *        level 2), 9 render (spectrogram.png).  fmcw_timing_read synchronises. */

@@ -1,3 +1,5 @@
+# STFT leg diagnostics (tools/stft_perf.py under the FMCW_STFT64_* knobs), PMC of the nfft-64
+# kernels, and one bench line.
 set -u
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
