@@ -850,9 +850,9 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   if (leg) {
     int st = FMCW_OK;
     bool fresh = false;
-    det_done = static_cast<int32_t*>(c->det_done.get(s, 4, &st, &fresh));
+    det_done = static_cast<int32_t*>(c->det_done.get(s, 9 * 128, &st, &fresh));   // 8 shards + top, 128 B apart
     CHK(st);
-    if (fresh) HIPCHK(hipMemsetAsync(det_done, 0, 4, s));
+    if (fresh) HIPCHK(hipMemsetAsync(det_done, 0, 9 * 128, s));
   }
   const int64_t pframe = probe_column > 0 ? (probe_column - 1) / C : -1;
   const int pchirp = probe_column > 0 ? (int)((probe_column - 1) % C) : 0;

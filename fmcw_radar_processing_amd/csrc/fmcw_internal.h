@@ -155,7 +155,7 @@ struct Detect1pArgs {
   // counts write-through and adds 1 to *done; the last one scans count_all[0..F_all) (the call's
   // earlier chunks included), writes list / *len, zeroes *pmax_reset (if set: the running max(P)
   // of the STFT passes that follow, :276 / :282) and resets *done for the next launch
-  int32_t* done;           // device counter, 0 before the first launch
+  int32_t* done;           // device counters, 0 before the first launch: 8 shards + the top, 32 words apart
   const int32_t* count_all;
   int64_t F_all;
   int pn;
@@ -202,8 +202,6 @@ struct StftArgs {
   int ncol;                // k_stft20 mode 3 / 4: columns in `bins`
   const int32_t* tiles;    // k_stft_mfma mode 1: the 256-segment tiles to cover (device), nullptr = all
   int ntiles;
-  int dbg;                 // diagnostic A/B knob of k_stft64m (FMCW_STFT64_DBG; wrong outputs): 1 no gather,
-                           // 2 no matrix products, 4 no output stores
 };
 
 // 20-tap fast path (kernels_stft.hip k_stft20): W table [nfft/2+1][20] from the window,

@@ -163,11 +163,20 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
   // the "one lane of each storing workgroup adds to ONE counter" row): sc1 stores, every storing
   // wave's vmcnt(0), a workgroup barrier, one agent-scope add; the last adder acquires and reads
   // the counts with sc1 loads.
+  // The arrivals are sharded (MI355X_MICROARCH.md fanin: ~12 ns per atomic on ONE word, ~12 us for
+  // the 1,024 workgroups of a 4096-frame launch): workgroup b adds to shard b % 8 (its own 128-byte
+  // line), the shard's last arriver adds to the top counter, and the top's last arriver scans.
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(a.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    const int G = (int)gridDim.x, sh = (int)(blockIdx.x & 7u);
+    const int in_shard = (G - sh + 7) / 8, shards = G < 8 ? G : 8;
+    int l = 0;
+    if (__hip_atomic_fetch_add(a.done + 32 * sh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_shard - 1)
+      l = __hip_atomic_fetch_add(a.done + 32 * 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == shards - 1;
+    last = l;
+  }
   __syncthreads();
   if (!last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -226,8 +235,8 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
   if (threadIdx.x == 0) {
     *a.len = carry * a.pn;
     if (a.pmax_reset) *a.pmax_reset = 0.f;
-    __hip_atomic_store(a.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (threadIdx.x < 9) __hip_atomic_store(a.done + 32 * threadIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------

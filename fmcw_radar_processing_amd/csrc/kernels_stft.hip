@@ -32,10 +32,13 @@ __device__ __forceinline__ void max_into(float* pmax, float m) {
 // psd = 20 log10(P / max) (:283) as 20 log10(2) log2(v): the hardware log2 (v_log_f32) and one
 // multiply, 3 instructions against log10f's 13 (which scales denormals and splits log10(2) for an
 // extra-precise product: < 1e-5 dB apart down to -200 dB, against the 1e-3 dB bar of SURVEY 8d).
-// Denormal v (below -759 dB) keeps log10f; v = 0 gives -Inf as MATLAB's G = 0 guard (:551).  Every
-// dB kernel uses it, so the matrix-core and VALU forms stay bit-identical.
+// A denormal v (below -759 dB) is scaled into the normal range first; v = 0 gives -Inf as MATLAB's
+// G = 0 guard (:551).  Every dB kernel uses it, so the matrix-core and VALU forms stay bit-identical.
 __device__ __forceinline__ float db20(float v) {
-  return v >= 1.17549435e-38f ? 6.0205999132796239f * __log2f(v) : 20.0f * log10f(v);
+  // branch-free: a denormal v is scaled by 2^32 into the normal range first (as OCML's log does)
+  const bool dn = v < 1.17549435e-38f;
+  const float l2 = __log2f(dn ? v * 4294967296.0f : v);
+  return fmaf(6.0205999132796239f, l2, dn ? -192.65919722494796f : 0.0f);
 }
 
 // ---------------------------------------------------------------------------
@@ -311,11 +314,6 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
   // division per tile, uniform; 32-bit ones per sample)
   const unsigned upn = (unsigned)a.pn;
   auto gather = [&](int64_t t, float (&v)[NPT]) __attribute__((always_inline)) {
-    if (a.dbg & 1) {
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) v[k] = (float)(threadIdx.x + k);
-      return;
-    }
     const int64_t s0 = t * TS;
     const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
     const int nsamp = (ns - 1) * a.hop + STFT_W;
@@ -379,7 +377,36 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
     if constexpr (MODE == 0) tile[sl * RS + b] = p;
     if constexpr (MODE == 2) tile[sl * RS + b] = db20(p * inv);    // :283
   };
-  float lmax = 0.f;
+  // P = |S|^2 * scale * g (g = 2 inside the one-sided spectrum, 1 at DC and Nyquist) as one multiply
+  // by scale * g: a power-of-two factor commutes with the rounding, so these are k_stft20's bits
+  const float sg0 = col == 0 ? scale : 2.f * scale, sg1 = 2.f * scale;
+  // max(P) of MODE 0 / 1 from the raw |S|^2 per lane (the scaling is monotonic: the same bits)
+  float m0 = 0.f, m1 = 0.f, mN = 0.f;
+  // one group's epilogue; FULL: the tile holds 256 segments (every tile but the last), no bounds checks
+  auto epilogue = [&](const f4t (&acc)[4], int sb, int ns, auto FULL) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int sl = sb + 4 * kq + r;
+      const float re0 = acc[0][r], im0 = col == 0 ? 0.f : acc[1][r];
+      const float q0 = fmaf(re0, re0, im0 * im0);
+      const float re1 = acc[2][r], im1 = acc[3][r];
+      const float q1 = fmaf(re1, re1, im1 * im1);
+      const float rn = acc[1][r];                                   // column 0: Re S of bin 32
+      const float qn = fmaf(rn, rn, 0.f * 0.f);
+      if (decltype(FULL)::value || sl < ns) {
+        if constexpr (MODE < 2) {
+          m0 = fmaxf(m0, q0);
+          m1 = fmaxf(m1, q1);
+          mN = fmaxf(mN, qn);
+        }
+        if constexpr (MODE != 1) {
+          emit(sl, col, q0 * sg0);
+          emit(sl, 16 + col, q1 * sg1);
+          if (col == 0) emit(sl, 32, qn * scale);
+        }
+      }
+    }
+  };
   // Persistent over tiles of 256 segments (grid: a few blocks per CU): the next tile's samples
   // are loaded while this one is transformed, so the gather's two dependent loads (frame list,
   // samples) and the block's start-up are paid once per block, not per tile
@@ -398,43 +425,17 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
       const int sb = w * 64 + 16 * g;
       if (sb >= ns) break;                                          // wave-uniform
       f4t acc[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if (a.dbg & 2) {
 #pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          const float av = xs[(sb + col) * a.hop + 4 * q + kq];
+      for (int q = 0; q < 5; ++q) {
+        const float av = xs[(sb + col) * a.hop + 4 * q + kq];
 #pragma unroll
-          for (int tt = 0; tt < 4; ++tt) acc[tt][q & 3] += av * bw[tt][q];
-        }
-      } else {
-#pragma unroll
-        for (int q = 0; q < 5; ++q) {
-          const float av = xs[(sb + col) * a.hop + 4 * q + kq];
-#pragma unroll
-          for (int tt = 0; tt < 4; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[tt][q], acc[tt], 0, 0, 0);
-        }
+        for (int tt = 0; tt < 4; ++tt) acc[tt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bw[tt][q], acc[tt], 0, 0, 0);
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int sl = sb + 4 * kq + r;
-        const float re0 = acc[0][r], im0 = col == 0 ? 0.f : acc[1][r];
-        const float p0 = fmaf(re0, re0, im0 * im0) * scale * (col == 0 ? 1.f : 2.f);
-        const float re1 = acc[2][r], im1 = acc[3][r];
-        const float p1 = fmaf(re1, re1, im1 * im1) * scale * 2.f;
-        const float rn = acc[1][r];                                 // column 0: Re S of bin 32
-        const float pn = fmaf(rn, rn, 0.f * 0.f) * scale;
-        if (sl < ns) {
-          if constexpr (MODE < 2) {
-            lmax = fmaxf(lmax, fmaxf(p0, p1));
-            if (col == 0) lmax = fmaxf(lmax, pn);
-          }
-          emit(sl, col, p0);
-          emit(sl, 16 + col, p1);
-          if (col == 0) emit(sl, 32, pn);
-        }
-      }
+      if (ns == TS) epilogue(acc, sb, ns, std::true_type{});
+      else epilogue(acc, sb, ns, std::false_type{});
     }
     __syncthreads();                                                // xs read out; the tile written
-    if (MODE != 1 && !(a.dbg & 4)) {
+    if constexpr (MODE != 1) {
       // the tile's rows s0 .. s0+ns-1 are one contiguous run of ns x 33 floats, 16-byte aligned
       // (s0 x 33 x 4 = 33792 t bytes): whole-line 16-byte stores
       float* out = (MODE == 0 ? a.P : dst) + s0 * NB;
@@ -453,6 +454,8 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
     }
   }
   if constexpr (MODE < 2) {
+    float lmax = fmaxf(m0 * sg0, m1 * sg1);
+    if (col == 0) lmax = fmaxf(lmax, mN * scale);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
     if (lane == 0) bmax[w] = lmax;
@@ -769,9 +772,6 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
     int bpc = 3;
     if (const char* e = std::getenv("FMCW_STFT64_BPC")) bpc = std::max(1, std::min(16, std::atoi(e)));   // A/B
     const unsigned g = (unsigned)std::min<int64_t>(blocks, (int64_t)cus * bpc);
-    StftArgs ad = a;
-    if (const char* e = std::getenv("FMCW_STFT64_DBG")) ad.dbg = std::atoi(e);   // diagnostics only
-    const StftArgs& a = ad;
     if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3(g), dim3(256), 0, s, a, tab, dst);
     else if (mode == 1) hipLaunchKernelGGL(k_stft64m<1>, dim3(g), dim3(256), 0, s, a, tab, dst);
     else hipLaunchKernelGGL(k_stft64m<2>, dim3(g), dim3(256), 0, s, a, tab, dst);
