@@ -218,6 +218,7 @@ hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_
 hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s, int64_t dst_cap,
                          int64_t tab_cap);
 
+
 struct StftDbArgs {
   const float* P;
   const int64_t* nseg;

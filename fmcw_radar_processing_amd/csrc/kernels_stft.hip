@@ -310,6 +310,8 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
   if ((int64_t)blockIdx.x >= ntiles) return;                        // block-uniform
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 15, kq = lane >> 4;
   const int nx = TS * a.hop + STFT_W;
+  // the tiles this block covers: t = blockIdx.x + k gridDim.x
+  const int64_t t_first = blockIdx.x;
   // sample q of the tile starting at q0: q < L is slow_mag[frame_list[q / pn]][q % pn] (one 64-bit
   // division per tile, uniform; 32-bit ones per sample)
   const unsigned upn = (unsigned)a.pn;
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
     }
   };
   float pre[NPT];
-  gather(blockIdx.x, pre);                                          // the first tile's samples in flight
+  if (t_first < ntiles) gather(t_first, pre);                       // the first tile's samples in flight
   // the table may be cached across calls (fmcw_api.cpp stft_tab64): it is used only when the 20
   // taps stored behind it are this call's window, else every lane forms its W entries itself
   // (the same fp64 expression as k_stft_table, so the same bits)
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
   // Persistent over tiles of 256 segments (grid: a few blocks per CU): the next tile's samples
   // are loaded while this one is transformed, so the gather's two dependent loads (frame list,
   // samples) and the block's start-up are paid once per block, not per tile
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  for (int64_t t = t_first; t < ntiles;) {
     const int64_t s0 = t * TS;
     const int ns = (int)(nseg - s0 < TS ? nseg - s0 : TS);
 #pragma unroll
@@ -418,7 +420,8 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
       const int i = threadIdx.x + 256 * k;
       if (i < nx) xs[i] = pre[k];
     }
-    if (t + gridDim.x < ntiles) gather(t + gridDim.x, pre);
+    const int64_t tn = t + gridDim.x;
+    if (tn < ntiles) gather(tn, pre);
     __syncthreads();                                                // xs holds tile t
 #pragma unroll 1
     for (int g = 0; g < 4; ++g) {                                   // 4 groups of 16 segments per wave
@@ -452,6 +455,7 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
       for (int o = 4 * n4 + threadIdx.x; o < n; o += 256) out[o] = tile[(o / NB) * RS + o % NB];
       __syncthreads();                                              // the tile read out
     }
+    t = tn;
   }
   if constexpr (MODE < 2) {
     float lmax = fmaxf(m0 * sg0, m1 * sg1);

@@ -173,3 +173,4 @@ def test_stft64_cached_table_follows_the_window(engine, direct):
     b2, mb2 = run()
     np.testing.assert_array_equal(b2, b1)
     assert mb == mb2
+
