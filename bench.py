@@ -61,10 +61,11 @@ def parse():
     ap.add_argument("--stream-frames", type=int, default=0,
                     help="BASELINE config 5: set --steps so that the run covers exactly this many frames over "
                          "all GPUs (65536 = the config-5 stream: 16 steps on 1 GPU, 2 on 8)")
-    ap.add_argument("--stft-form", choices=["direct", "stored"], default="stored",
-                    help="dB of the STFT leg: stored = pass 1 writes P and max(P), pass 2 turns P into dB in "
-                         "place (0.103 ms per step); direct = pass 1 max(P) only, pass 2 recomputes P and writes "
-                         "dB, P never stored (0.124 ms; profiles/r04g_stft_ab.txt)")
+    ap.add_argument("--stft-form", choices=["direct", "stored"], default="direct",
+                    help="dB of the STFT leg: direct = pass 1 max(P) only, pass 2 recomputes P and writes dB, "
+                         "P never stored (round 5, the folded k_stft64f: 0.077 ms per step); stored = pass 1 "
+                         "writes P and max(P), pass 2 turns P into dB in place (0.084 ms; "
+                         "profiles/r05_stft_fold.txt)")
     ap.add_argument("--no-copy-ceiling", action="store_true",
                     help="skip the in-run HBM copy ceiling of k_rdx's bytes (roofline.copy_ceiling_ms)")
     ap.add_argument("--dry-dist", action="store_true",

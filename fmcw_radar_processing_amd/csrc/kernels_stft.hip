@@ -12,6 +12,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include "fmcw_internal.h"
 #include "../../include/fmcw.h"
 
@@ -472,6 +474,281 @@ __global__ __launch_bounds__(256) void k_stft64m(StftArgs a, const float2* __res
 }
 
 // ---------------------------------------------------------------------------
+// The nfft-64 STFT folded about the window's centre (round 5; the default for config 4).  For
+// the segment x[s .. s+19] and theta_b = 2 pi b / 64, pairing tap 10+k with tap 9-k (k = 0..9):
+//   S(b) e^{i theta_b 9.5} = sum_k (u_k cos(theta_b (k + 1/2)) - i v_k sin(theta_b (k + 1/2))),
+//   u_k = w[10+k] x[s+10+k] + w[9-k] x[s+9-k],  v_k = w[10+k] x[s+10+k] - w[9-k] x[s+9-k],
+// and P only needs |S|^2, which the phase factor leaves unchanged: two 10-term real sums per bin
+// instead of one 20-term complex one, for any window (the taps are applied to the samples).  Per
+// 32 segments: [32 seg x 10] x [10 x 32 bins] twice, 2 x 5 v_mfma_f32_32x32x2_f32 (k_stft64m: 20
+// v_mfma_f32_16x16x4_f32 per 16 segments, 2.5x the matrix work).  Re from the sums u, Im from the
+// differences v; Im of bin 0 is identically 0, so its column carries the Nyquist bin (cos terms
+// 0, sin terms (-1)^k, exact).  Not bit-identical to k_stft20 (a different exact identity, the
+// same f32 error order: tests/test_gpu_stft_mfma.py holds it to the VALU form and the oracle).
+// Lane l: A = u or v of segment sb + (l & 31), k = 2q + (l >> 5); B = cos / sin of bin l & 31 at
+// that k; result register r: segment sb + (r & 3) + 8 (r >> 2) + 4 (l >> 5), bin l & 31.
+// Each wave is independent (no block barrier in the loop): units of 64 segments, the next unit's
+// samples gathered into registers while this one is transformed, its outputs staged in the
+// wave's own LDS tile in the output's [seg][33] layout and stored as 16-byte lines.
+// ---------------------------------------------------------------------------
+// cos(pi m / 64), m = 0..127, correctly rounded (exact zeros at m = 32, 96): the folded form's B
+// operands are cos / sin (pi b (2k+1) / 64) = k_cospi64[b (2k+1) mod 128] / k_cospi64[(b (2k+1) - 32) mod 128]
+__device__ const float k_cospi64[128] = {
+    0x1.0000000000000p+0f, 0x1.ff621e0000000p-1f, 0x1.fd88da0000000p-1f, 0x1.fa75580000000p-1f,
+    0x1.f6297c0000000p-1f, 0x1.f0a7f00000000p-1f, 0x1.e9f4160000000p-1f, 0x1.e212100000000p-1f,
+    0x1.d906bc0000000p-1f, 0x1.ced7b00000000p-1f, 0x1.c38b300000000p-1f, 0x1.b728340000000p-1f,
+    0x1.a9b6620000000p-1f, 0x1.9b3e040000000p-1f, 0x1.8bc8060000000p-1f, 0x1.7b5df20000000p-1f,
+    0x1.6a09e60000000p-1f, 0x1.57d6940000000p-1f, 0x1.44cf320000000p-1f, 0x1.30ff800000000p-1f,
+    0x1.1c73b40000000p-1f, 0x1.07387a0000000p-1f, 0x1.e2b5d40000000p-2f, 0x1.b5d1000000000p-2f,
+    0x1.87de2a0000000p-2f, 0x1.58f9a80000000p-2f, 0x1.2940620000000p-2f, 0x1.f19f980000000p-3f,
+    0x1.8f8b840000000p-3f, 0x1.2c81060000000p-3f, 0x1.917a6c0000000p-4f, 0x1.91f6600000000p-5f,
+    0.0f, -0x1.91f6600000000p-5f, -0x1.917a6c0000000p-4f, -0x1.2c81060000000p-3f,
+    -0x1.8f8b840000000p-3f, -0x1.f19f980000000p-3f, -0x1.2940620000000p-2f, -0x1.58f9a80000000p-2f,
+    -0x1.87de2a0000000p-2f, -0x1.b5d1000000000p-2f, -0x1.e2b5d40000000p-2f, -0x1.07387a0000000p-1f,
+    -0x1.1c73b40000000p-1f, -0x1.30ff800000000p-1f, -0x1.44cf320000000p-1f, -0x1.57d6940000000p-1f,
+    -0x1.6a09e60000000p-1f, -0x1.7b5df20000000p-1f, -0x1.8bc8060000000p-1f, -0x1.9b3e040000000p-1f,
+    -0x1.a9b6620000000p-1f, -0x1.b728340000000p-1f, -0x1.c38b300000000p-1f, -0x1.ced7b00000000p-1f,
+    -0x1.d906bc0000000p-1f, -0x1.e212100000000p-1f, -0x1.e9f4160000000p-1f, -0x1.f0a7f00000000p-1f,
+    -0x1.f6297c0000000p-1f, -0x1.fa75580000000p-1f, -0x1.fd88da0000000p-1f, -0x1.ff621e0000000p-1f,
+    -0x1.0000000000000p+0f, -0x1.ff621e0000000p-1f, -0x1.fd88da0000000p-1f, -0x1.fa75580000000p-1f,
+    -0x1.f6297c0000000p-1f, -0x1.f0a7f00000000p-1f, -0x1.e9f4160000000p-1f, -0x1.e212100000000p-1f,
+    -0x1.d906bc0000000p-1f, -0x1.ced7b00000000p-1f, -0x1.c38b300000000p-1f, -0x1.b728340000000p-1f,
+    -0x1.a9b6620000000p-1f, -0x1.9b3e040000000p-1f, -0x1.8bc8060000000p-1f, -0x1.7b5df20000000p-1f,
+    -0x1.6a09e60000000p-1f, -0x1.57d6940000000p-1f, -0x1.44cf320000000p-1f, -0x1.30ff800000000p-1f,
+    -0x1.1c73b40000000p-1f, -0x1.07387a0000000p-1f, -0x1.e2b5d40000000p-2f, -0x1.b5d1000000000p-2f,
+    -0x1.87de2a0000000p-2f, -0x1.58f9a80000000p-2f, -0x1.2940620000000p-2f, -0x1.f19f980000000p-3f,
+    -0x1.8f8b840000000p-3f, -0x1.2c81060000000p-3f, -0x1.917a6c0000000p-4f, -0x1.91f6600000000p-5f,
+    0.0f, 0x1.91f6600000000p-5f, 0x1.917a6c0000000p-4f, 0x1.2c81060000000p-3f,
+    0x1.8f8b840000000p-3f, 0x1.f19f980000000p-3f, 0x1.2940620000000p-2f, 0x1.58f9a80000000p-2f,
+    0x1.87de2a0000000p-2f, 0x1.b5d1000000000p-2f, 0x1.e2b5d40000000p-2f, 0x1.07387a0000000p-1f,
+    0x1.1c73b40000000p-1f, 0x1.30ff800000000p-1f, 0x1.44cf320000000p-1f, 0x1.57d6940000000p-1f,
+    0x1.6a09e60000000p-1f, 0x1.7b5df20000000p-1f, 0x1.8bc8060000000p-1f, 0x1.9b3e040000000p-1f,
+    0x1.a9b6620000000p-1f, 0x1.b728340000000p-1f, 0x1.c38b300000000p-1f, 0x1.ced7b00000000p-1f,
+    0x1.d906bc0000000p-1f, 0x1.e212100000000p-1f, 0x1.e9f4160000000p-1f, 0x1.f0a7f00000000p-1f,
+    0x1.f6297c0000000p-1f, 0x1.fa75580000000p-1f, 0x1.fd88da0000000p-1f, 0x1.ff621e0000000p-1f,
+};
+
+template <int MODE, bool H1>
+__global__ __launch_bounds__(256) void k_stft64f(StftArgs a, float* __restrict__ dst) {
+  // US segments per unit; a wave gathers UB units' samples at once (every load of the batch in
+  // flight together: the frame-list loads first, then the samples), then transforms them in turn
+  constexpr int US = 64, NB = 33, UB = 4, HOPMAX = H1 ? 1 : 4;
+  constexpr int NXW = US * HOPMAX + STFT_W, NPW = (NXW + 63) / 64;
+  typedef float f16t __attribute__((ext_vector_type(16)));
+  typedef float f4t __attribute__((ext_vector_type(4)));
+  __shared__ float xs_all[4][UB * NXW];
+  __shared__ __attribute__((aligned(16))) float tile_all[MODE == 1 ? 1 : 4][MODE == 1 ? 4 : US * NB];
+  __shared__ float bmax[4];
+  const int hop = H1 ? 1 : a.hop;
+  const int64_t L = *a.len;
+  const int64_t H = a.halo_len ? *a.halo_len : a.n_halo;
+  const int64_t Lx = L + H;
+  const int noverlap = STFT_W - hop;
+  int64_t nseg = Lx - noverlap >= 0 ? (Lx - noverlap) / hop : 0;     // fix((L-noverlap)/hop)
+  if (nseg > a.max_seg) nseg = a.max_seg;
+  if (MODE < 2 && blockIdx.x == 0 && threadIdx.x == 0) *a.nseg_out = nseg;
+#ifdef STFT_AB_STAMPS   // development probe (tools/stft_stamps.py): the max(P) pass's s_memtime / s_memrealtime stamps into a caller-sized nseg_out
+  unsigned long long* stp = reinterpret_cast<unsigned long long*>(a.nseg_out) + 1;
+  const bool stamper = MODE == 1 && threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1);
+  const int so = blockIdx.x == 0 ? 0 : 16;
+  int nst = 0;
+#define STAMP() do { if (stamper && nst < 15) { stp[so + nst] = __builtin_amdgcn_s_memtime(); } ++nst; } while (0)
+  unsigned long long* rtp = reinterpret_cast<unsigned long long*>(a.nseg_out) + 64 + 3 * (blockIdx.x * 4 + (threadIdx.x >> 6));
+  if (MODE == 1 && (threadIdx.x & 63) == 0) { rtp[0] = __builtin_amdgcn_s_memrealtime(); unsigned xcc, hwid; asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc)); asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid)); rtp[2] = ((unsigned long long)xcc << 32) | hwid; }
+#else
+#define STAMP() do {} while (0)
+#endif
+  STAMP();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, col = lane & 31, kh = lane >> 5;
+  float* xs = xs_all[w];
+  float* tile = tile_all[MODE == 1 ? 0 : w];
+  const int64_t units = (nseg + US - 1) / US;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const unsigned upn = (unsigned)a.pn;
+  // sample i of unit u: q = 64 u hop + i; q < L is slow_mag[frame_list[q / pn]][q % pn], L <= q <
+  // L + H the halo, past the unit's last segment 0.  q0 / pn once per unit from a double reciprocal
+  // (exact after one correction step: q0 < 2^53), (q0 % pn + i) / pn per sample from a float one
+  // (exact after one correction step: the dividend is below pn + 276 < 2^24); no integer division
+  const double inv_pn_d = 1.0 / (double)a.pn;
+  const float inv_pn_f = 1.0f / (float)a.pn;
+  auto locate = [&](int64_t u, int (&f)[NPW], unsigned (&c)[NPW]) __attribute__((always_inline)) {
+    const int64_t s0 = u * US;
+    const int ns = (int)(nseg - s0 < US ? nseg - s0 : US);
+    const int nsamp = u < units ? (ns - 1) * hop + STFT_W : 0;
+    const int64_t q0 = s0 * hop;
+    int64_t fq0 = (int64_t)((double)q0 * inv_pn_d);
+    int64_t r0 = q0 - fq0 * a.pn;
+    if (r0 < 0) { --fq0; r0 += a.pn; }
+    if (r0 >= a.pn) { ++fq0; r0 -= a.pn; }
+#pragma unroll
+    for (int k = 0; k < NPW; ++k) {
+      const int i = lane + 64 * k;
+      f[k] = -2;
+      c[k] = 0;
+      if (i < nsamp) {
+        const int64_t q = q0 + i;
+        if (q < L) {
+          const unsigned rr = (unsigned)r0 + (unsigned)i;
+          unsigned df = (unsigned)((float)rr * inv_pn_f);
+          int d = (int)(rr - df * upn);
+          if (d < 0) { --df; d += a.pn; }
+          if (d >= a.pn) { ++df; d -= a.pn; }
+          f[k] = a.frame_list[fq0 + df];
+          c[k] = (unsigned)d;
+        } else {
+          f[k] = -1;
+          c[k] = (unsigned)(q - L);
+        }
+      }
+    }
+  };
+  // this lane's taps (k = 2q + kh) and B operands
+  float wp[5], wn[5], bc[5], bs[5];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const int k = 2 * q + kh;
+    wp[q] = a.win[10 + k];
+    wn[q] = a.win[9 - k];
+    const int m = (col * (2 * k + 1)) & 127;
+    bc[q] = k_cospi64[m];
+    bs[q] = col == 0 ? ((k & 1) ? -1.f : 1.f) : k_cospi64[(m + 96) & 127];   // column 0: the Nyquist bin's sin terms
+  }
+  float usum = 0.f;
+#pragma unroll
+  for (int m = 0; m < STFT_W; ++m) usum = fmaf(a.win[m], a.win[m], usum);
+  const float scale = a.inv_fs / usum;                              // 1/(fs*sum(w.^2))
+  float inv = 0.f;
+  if constexpr (MODE == 2) {
+    const float pm = *a.pmax;
+    inv = pm > 0.f ? 1.0f / pm : 0.f;                               // all-zero P: -Inf dB (MATLAB G = 0)
+  }
+  // P = |S|^2 * scale * g (g = 2 inside the one-sided spectrum, 1 at DC and Nyquist); MODE 2 writes
+  // P / max(P) = |S|^2 * (scale g / max(P)) into the tile and takes 20 log10 in the store phase
+  const float sg = col == 0 ? scale : 2.f * scale;
+  const float fz = col == 0 ? 0.f : 1.f;                            // column 0: Im S of bin 0 is 0
+  const int nyo = col == 0 ? 32 : col;                              // column 0 also writes the Nyquist bin
+  const float so = MODE == 2 ? sg * inv : sg, sn = MODE == 2 ? scale * inv : scale;
+  // max of the raw |S|^2 as unsigned bits (|S|^2 >= 0: the order of the bits is the order of the
+  // values, one v_max_u32 and no NaN quieting); the scaling is monotonic, so max(P) = max(|S|^2) g scale
+  unsigned m0 = 0u, mN = 0u;
+  // one group's epilogue; FULL: all 64 segments of the unit exist (every unit but the last), no checks
+  auto epilogue = [&](const f16t& re, const f16t& im, int sb, int ns, auto FULL) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int sl = sb + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      const float rv = re[r], iv = im[r];
+      const float t = iv * iv;                                      // column 0: |S|^2 of the Nyquist bin
+      const float q = fmaf(rv, rv, t * fz);                         // |S|^2 of bin col
+      if (decltype(FULL)::value || sl < ns) {
+        if constexpr (MODE < 2) {
+          m0 = max(m0, __float_as_uint(q));
+          mN = max(mN, __float_as_uint(t));
+        }
+        if constexpr (MODE != 1) {
+          const float p = q * so;
+          tile[sl * NB + col] = p;
+          tile[sl * NB + nyo] = col == 0 ? t * sn : p;              // column 0: the Nyquist bin, else p again
+        }
+      }
+    }
+  };
+  STAMP();
+  for (int64_t ub = (int64_t)blockIdx.x * 4 + w; ub < units; ub += UB * nw) {
+    int fr[UB][NPW];
+    unsigned cc[UB][NPW];
+    float xv[UB][NPW];
+#pragma unroll
+    for (int b = 0; b < UB; ++b) locate(ub + b * nw, fr[b], cc[b]);
+#pragma unroll
+    for (int b = 0; b < UB; ++b)
+#pragma unroll
+      for (int k = 0; k < NPW; ++k) {
+        const int f = fr[b][k];
+        xv[b][k] = f >= 0 ? a.slow_mag[(int64_t)f * a.pn + cc[b][k]] : f == -1 ? a.halo[cc[b][k]] : 0.f;
+      }
+#pragma unroll
+    for (int b = 0; b < UB; ++b)
+#pragma unroll
+      for (int k = 0; k < NPW; ++k) {
+        const int i = lane + 64 * k;
+        if (i < NXW) xs[b * NXW + i] = xv[b][k];
+      }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");          // xs written before any lane reads it
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    STAMP();
+#pragma unroll 1
+    for (int b = 0; b < UB; ++b) {
+      const int64_t u = ub + b * nw;
+      if (u >= units) break;                                        // wave-uniform
+      const int64_t s0 = u * US;
+      const int ns = (int)(nseg - s0 < US ? nseg - s0 : US);
+      const float* xb = xs + b * NXW;
+#pragma unroll 1
+      for (int g = 0; g < 2; ++g) {
+        const int sb = 32 * g;
+        if (sb >= ns) break;                                        // wave-uniform
+        f16t re = {}, im = {};
+        const int base = (sb + col) * hop;
+#pragma unroll
+        for (int q = 0; q < 5; ++q) {
+          const int k = 2 * q + kh;
+          const float xp = xb[base + 10 + k], xm = xb[base + 9 - k];
+          const float t = wn[q] * xm;
+          const float uk = fmaf(wp[q], xp, t), vk = fmaf(wp[q], xp, -t);
+          re = __builtin_amdgcn_mfma_f32_32x32x2f32(uk, bc[q], re, 0, 0, 0);
+          im = __builtin_amdgcn_mfma_f32_32x32x2f32(vk, bs[q], im, 0, 0, 0);
+        }
+        if (ns == US) epilogue(re, im, sb, ns, std::true_type{});
+        else epilogue(re, im, sb, ns, std::false_type{});
+      }
+      if constexpr (MODE != 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");      // the tile written before it is read out
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // rows s0 .. s0+ns-1 are one contiguous run of ns x 33 floats, 16-byte aligned (s0 x 132 = 8448 u bytes)
+        float* out = (MODE == 0 ? a.P : dst) + s0 * NB;
+        const int n = ns * NB, n4 = n >> 2;
+        const f4t* t4 = reinterpret_cast<const f4t*>(tile);
+        if constexpr (MODE == 0) {
+          for (int i = lane; i < n4; i += 64) reinterpret_cast<f4t*>(out)[i] = t4[i];
+          for (int o = 4 * n4 + lane; o < n; o += 64) out[o] = tile[o];
+        } else {                                                    // :283 20 log10(P / max(P))
+          for (int i = lane; i < n4; i += 64) {
+            const f4t v = t4[i];
+            reinterpret_cast<f4t*>(out)[i] = f4t{db20(v.x), db20(v.y), db20(v.z), db20(v.w)};
+          }
+          for (int o = 4 * n4 + lane; o < n; o += 64) out[o] = db20(tile[o]);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");      // read out before the next unit rewrites it
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+    STAMP();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");          // xs read before the next batch rewrites it
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  STAMP();
+#ifdef STFT_AB_STAMPS
+  if (MODE == 1 && (threadIdx.x & 63) == 0) rtp[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if constexpr (MODE < 2) {
+    float lmax = __uint_as_float(m0) * sg;
+    if (col == 0) lmax = fmaxf(lmax, __uint_as_float(mN) * scale);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    if (lane == 0) bmax[w] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const float m = fmaxf(fmaxf(bmax[0], bmax[1]), fmaxf(bmax[2], bmax[3]));
+      max_into(a.pmax, m);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_stft20 on the matrix cores for any nfft (the host call's reference rule nfft =
 // 2^nextpow2(L), :273, e.g. 65536 for 256 config-3 frames): columns in chunks of 32 bins,
 // tiles 0 / 1 = Re / Im W of the chunk's bins 0-15, tiles 2 / 3 = bins 16-31, 5 k-steps of
@@ -775,6 +1052,36 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
     }
     int bpc = 3;
     if (const char* e = std::getenv("FMCW_STFT64_BPC")) bpc = std::max(1, std::min(16, std::atoi(e)));   // A/B
+    const char* fe = std::getenv("FMCW_STFT64_FOLD");
+    if (!(fe && fe[0] == '0')) {                  // the folded form (default; =0: k_stft64m, bit-identical to k_stft20)
+      // persistent: exactly the blocks that are resident at once (the occupancy query of each
+      // instantiation, once): a grid past it runs its last blocks as a second round, which cost
+      // the first form of this kernel 2x (3 resident blocks per CU against the 4 launched)
+      const void* kf = a.hop == 1 ? (mode == 0 ? (const void*)k_stft64f<0, true> : mode == 1 ? (const void*)k_stft64f<1, true>
+                                                                                           : (const void*)k_stft64f<2, true>)
+                                  : (mode == 0 ? (const void*)k_stft64f<0, false> : mode == 1 ? (const void*)k_stft64f<1, false>
+                                                                                              : (const void*)k_stft64f<2, false>);
+      static std::mutex mu;
+      static std::map<const void*, int> occ;
+      int bpcf;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = occ.find(kf);
+        if (it == occ.end()) {
+          int n = 0;
+          if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kf, 256, 0) != hipSuccess || n < 1) n = 1;
+          it = occ.emplace(kf, n).first;
+        }
+        bpcf = it->second;
+      }
+      if (const char* e = std::getenv("FMCW_STFT64_BPC")) bpcf = std::max(1, std::min(8, std::atoi(e)));   // A/B
+      const int64_t wblocks = (a.max_seg + 255) / 256;                  // 4 waves x 64 segments per block and pass
+      const unsigned g = (unsigned)std::min<int64_t>(wblocks, (int64_t)cus * bpcf);
+      StftArgs ka = a;
+      float* kd = dst;
+      void* args[] = {&ka, &kd};
+      return hipLaunchKernel(kf, dim3(g), dim3(256), args, 0, s);
+    }
     const unsigned g = (unsigned)std::min<int64_t>(blocks, (int64_t)cus * bpc);
     if (mode == 0) hipLaunchKernelGGL(k_stft64m<0>, dim3(g), dim3(256), 0, s, a, tab, dst);
     else if (mode == 1) hipLaunchKernelGGL(k_stft64m<1>, dim3(g), dim3(256), 0, s, a, tab, dst);

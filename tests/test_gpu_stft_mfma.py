@@ -1,5 +1,7 @@
-"""The nfft-64 STFT on the matrix cores (k_stft64m, kernels_stft.hip) against the VALU k_stft20
-it replaces for config 4: P (:276, one-sided 'psd'), max(P) (:282) and the direct 20 log10(P / max) (:283) bit for bit.
+"""The STFT on the matrix cores against the VALU k_stft20 it replaces: P (:276, one-sided 'psd'),
+max(P) (:282) and the direct 20 log10(P / max) (:283) bit for bit for k_stft_mfma (any nfft) and
+k_stft64m (nfft 64, FMCW_STFT64_FOLD=0); the folded nfft-64 form k_stft64f (the default for
+config 4: taps 10+k and 9-k paired, half the matrix work) to the fp32 dB bar.
 
 An f32 MFMA is a k-ordered chain of f32 fmas, so each S(seg, bin) is the same chain over the
 20 taps as k_stft20's loop; FMCW_STFT_MFMA=0 selects the VALU kernel.  nfft 64 runs the
@@ -16,15 +18,16 @@ pytestmark = pytest.mark.gpu
 WLEN, NFFT, PN = 20, 64, 256
 
 
-def _run(engine, monkeypatch, mfma, x, hop, halo, store, nfft=NFFT):
+def _run(engine, monkeypatch, mfma, x, hop, halo, store, nfft=NFFT, fold=False, win=None):
     import torch
     monkeypatch.setenv("FMCW_STFT_MFMA", "1" if mfma else "0")
+    monkeypatch.setenv("FMCW_STFT64_FOLD", "1" if fold else "0")
     dev = "cuda"
     nfr = len(x) // PN
     slow = torch.from_numpy(x.reshape(nfr, PN)).to(dev)
     flist = torch.arange(nfr, dtype=torch.int32, device=dev)
     d_len = torch.tensor([len(x)], dtype=torch.int64, device=dev)
-    win = torch.from_numpy(np.hanning(WLEN + 2)[1:-1].astype(np.float32)).to(dev)
+    win = torch.from_numpy((np.hanning(WLEN + 2)[1:-1] if win is None else win).astype(np.float32)).to(dev)
     max_seg = len(x) + WLEN
     d_P = torch.full((max_seg, nfft // 2 + 1), np.nan, dtype=torch.float32, device=dev)
     pmax = torch.zeros(1, dtype=torch.float32, device=dev)
@@ -54,9 +57,57 @@ def test_mfma_stft_is_bit_identical(engine, monkeypatch, frames, hop, halo, stor
     x = (np.repeat(rng.uniform(0.5, 40.0, frames), PN) * (1 + 0.05 * rng.standard_normal(frames * PN))).astype(np.float32)
     x = np.abs(x)
     hl = (np.abs(rng.standard_normal(WLEN - 1)) * 20).astype(np.float32) if halo else None
-    n1, p1, m1 = _run(engine, monkeypatch, True, x, hop, hl, store, nfft)
+    n1, p1, m1 = _run(engine, monkeypatch, True, x, hop, hl, store, nfft)     # k_stft64m at nfft 64
     n0, p0, m0 = _run(engine, monkeypatch, False, x, hop, hl, store, nfft)
     assert n1 == n0 and n1 == (len(x) + (WLEN - 1 if halo else 0) - (WLEN - hop)) // hop
     np.testing.assert_array_equal(m1, m0)
     assert not np.isnan(p1).any()
     np.testing.assert_array_equal(p1, p0)        # P (stored pass) or the dB map (direct pass)
+
+
+def _db(p, pm):
+    with np.errstate(divide="ignore"):
+        return 20 * np.log10(p.astype(np.float64) / np.float64(pm))   # :283 20 log10 of the power
+
+
+def _truth_db(x, halo, w, hop):
+    """fp64 P of every segment and bin (the 64-point DFT of the windowed 20-sample segment, one-sided
+    'psd' scaling), as dB against its own maximum."""
+    xx = np.concatenate([x, halo]) if halo is not None else x
+    xx = xx.astype(np.float64)
+    ns = (len(xx) - (WLEN - hop)) // hop
+    X = np.lib.stride_tricks.sliding_window_view(xx, WLEN)[::hop][:ns]
+    S = (X * w.astype(np.float32).astype(np.float64)) @ np.exp(-2j * np.pi * np.outer(np.arange(WLEN), np.arange(33)) / 64)
+    P = np.abs(S) ** 2
+    P[:, 1:32] *= 2
+    return _db(P, P.max())
+
+
+@pytest.mark.parametrize("frames,hop,halo,store,wkind", [(3, 1, False, True, "hann"), (7, 1, True, True, "hann"),
+                                                          (5, 3, False, True, "kaiser"), (9, 1, False, False, "hann"),
+                                                          (40, 1, False, False, "kaiser"), (2, 4, False, False, "rand"),
+                                                          (4, 1, True, False, "rand")])
+def test_folded_stft64_meets_the_db_bar(engine, monkeypatch, frames, hop, halo, store, wkind):
+    """k_stft64f (default at nfft 64) against fp64: every output at or above -80 dB within 1e-3 dB
+    (the fp32 STFT bar of tests/test_gpu_device_path.py), the bins below the floor finite and below
+    it, max(P) within 2e-6 of k_stft20's (VALU).  The two fp32 forms differ from each other by up to
+    twice the bar near the floor (each is within it of fp64), so they are not compared with each
+    other.  Windows that are not bit-symmetric (kaiser(20, 3), a random one) included: the fold
+    applies the taps to the samples, so it needs no symmetry."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(frames * 7 + hop)
+    x = (np.repeat(rng.uniform(0.5, 40.0, frames), PN) * (1 + 0.05 * rng.standard_normal(frames * PN))).astype(np.float32)
+    x = np.abs(x)
+    hl = (np.abs(rng.standard_normal(WLEN - 1)) * 20).astype(np.float32) if halo else None
+    w = {"hann": O.stft_window("hann"), "kaiser": O.stft_window("kaiser"), "rand": rng.uniform(0.1, 1.0, WLEN)}[wkind]
+    n1, p1, m1 = _run(engine, monkeypatch, True, x, hop, hl, store, 64, fold=True, win=w)
+    n0, p0, m0 = _run(engine, monkeypatch, False, x, hop, hl, store, 64, win=w)
+    assert n1 == n0 == (len(x) + (WLEN - 1 if halo else 0) - (WLEN - hop)) // hop
+    assert abs(float(m1[0]) / float(m0[0]) - 1) <= 2e-6
+    d1 = _db(p1, m1[0]) if store else p1.astype(np.float64)
+    dt = _truth_db(x, hl, w, hop)
+    assert dt.shape == d1.shape
+    sel = dt >= -80
+    assert sel.mean() > 0.2
+    assert np.abs(d1[sel] - dt[sel]).max() <= 1e-3
+    assert (d1[~sel] <= -80 + 1e-3).all() and not np.isnan(d1).any()
