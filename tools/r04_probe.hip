@@ -236,7 +236,9 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
 // read of the slot's previous unit is done), then loads the next unit's input.  2 slots.
 // LAGP: the unit polled and loaded in step j is j - LAGP (1: k_rdx); NS >= 2 LAGP slots (a member
 // that sees ready(j - LAGP) knows every member has read unit j - 2 LAGP)
-template <int UC, int LAGP = 1, int NS = 2, int HB = 1>   // HB 2: every stream at half the bytes (fp16 storage, part K)
+// BURN (part M, round 5): v_pk_fma_f32 per wave and full-frame step (scaled by UC / 256) after
+// R(j)'s slot stores, with the next input loads in flight -- k_rdx's DSP energy without its data
+template <int UC, int LAGP = 1, int NS = 2, int HB = 1, int BURN = 0>   // HB 2: every stream at half the bytes (fp16 storage, part K)
 __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
                                                      unsigned* ctr, long nunits, unsigned* err) {
   constexpr int THR = 512;
@@ -304,6 +306,20 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
         __builtin_amdgcn_raw_buffer_store_b128(xin[i], rs, (((p >> 4) * UC + ch) * 16 + (p & 15)) * 16, 0, 0);
       }
       if (j + 1 < nj) ld_in(j + 1, xin);
+      if constexpr (BURN > 0) {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        f2 u[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) u[i] = f2{acc.x + (float)i, acc.y - (float)i};
+        const f2 m{acc.z * 1e-30f + 0.999f, acc.w * 1e-30f + 0.998f}, c{1e-3f, 2e-3f};
+        constexpr int IT = BURN * UC / 256 / 8;
+#pragma unroll 4
+        for (int it = 0; it < IT; ++it)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) u[i] = __builtin_elementwise_fma(u[i], m, c);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc.x += u[i].x + u[i].y;
+      }
     }
   }
   if (acc.x == 1234.5f) rd[tid] = 1;
@@ -669,6 +685,17 @@ int main(int argc, char** argv) {
     rb("roles, 2 slots", teamx(k_team_role<2>, 256));
     rb("roles, 3 slots", teamx(k_team_role<3>, 256));
     rb("roles, 4 slots", teamx(k_team_role<4>, 256));
+  }
+  if (part == 13) {
+    printf("== part M: k_rdx's protocol under a VALU burn (v_pk_fma_f32 per wave and frame step; k_rdx: ~1,000 VALU)\n");
+    rb("frame, lag 1, 2 slots, burn 0", teamd(k_team_def<256, 1, 2, 1, 0>, 256));
+    rb("half, lag 2, 4 slots, burn 0", teamd(k_team_def<128, 2, 4, 1, 0>, 128));
+    rb("frame, lag 1, 2 slots, burn 768", teamd(k_team_def<256, 1, 2, 1, 768>, 256));
+    rb("half, lag 2, 4 slots, burn 768", teamd(k_team_def<128, 2, 4, 1, 768>, 128));
+    rb("frame, lag 1, 2 slots, burn 1536", teamd(k_team_def<256, 1, 2, 1, 1536>, 256));
+    rb("half, lag 2, 4 slots, burn 1536", teamd(k_team_def<128, 2, 4, 1, 1536>, 128));
+    rb("frame, lag 1, 2 slots, burn 3072", teamd(k_team_def<256, 1, 2, 1, 3072>, 256));
+    rb("half, lag 2, 4 slots, burn 3072", teamd(k_team_def<128, 2, 4, 1, 3072>, 128));
   }
   if (part == 11) {
     printf("== part K: k_rdx's protocol at fp16-storage bytes (input, RD and slots halved; frac on 8.6 GB)\n");
