@@ -238,7 +238,7 @@ __global__ __launch_bounds__(THR, 1) void k_team(const char* __restrict__ iq, ch
 // that sees ready(j - LAGP) knows every member has read unit j - 2 LAGP)
 // BURN (part M, round 5): v_pk_fma_f32 per wave and full-frame step (scaled by UC / 256) after
 // R(j)'s slot stores, with the next input loads in flight -- k_rdx's DSP energy without its data
-template <int UC, int LAGP = 1, int NS = 2, int HB = 1, int BURN = 0>   // HB 2: every stream at half the bytes (fp16 storage, part K)
+template <int UC, int LAGP = 1, int NS = 2, int HB = 1, int BURN = 0, int BURNK = 0>   // HB 2: every stream at half the bytes (fp16 storage, part K)
 __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq, char* __restrict__ cube, char* __restrict__ rd,
                                                      unsigned* ctr, long nunits, unsigned* err) {
   constexpr int THR = 512;
@@ -307,16 +307,22 @@ __global__ __launch_bounds__(512, 1) void k_team_def(const char* __restrict__ iq
       }
       if (j + 1 < nj) ld_in(j + 1, xin);
       if constexpr (BURN > 0) {
+        // BURNK 0: u = 0.999 u + c (converges: constant bits, little switching); 1: u = -0.5 u + g with
+        // g the random samples of the group (every mantissa bit toggles, as in the FFTs)
         typedef float f2 __attribute__((ext_vector_type(2)));
-        f2 u[8];
+        f2 u[8], g[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) u[i] = f2{acc.x + (float)i, acc.y - (float)i};
-        const f2 m{acc.z * 1e-30f + 0.999f, acc.w * 1e-30f + 0.998f}, c{1e-3f, 2e-3f};
+        for (int i = 0; i < 8; ++i) {
+          u[i] = f2{acc.x + (float)i, acc.y - (float)i};
+          const f4v gi = grp[i % NL];
+          g[i] = i & 1 ? f2{gi.z, gi.w} : f2{gi.x, gi.y};
+        }
+        const f2 m = BURNK ? f2{-0.5f, -0.5f} : f2{acc.z * 1e-30f + 0.999f, acc.w * 1e-30f + 0.998f};
         constexpr int IT = BURN * UC / 256 / 8;
 #pragma unroll 4
         for (int it = 0; it < IT; ++it)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) u[i] = __builtin_elementwise_fma(u[i], m, c);
+          for (int i = 0; i < 8; ++i) u[i] = __builtin_elementwise_fma(u[i], m, BURNK ? g[(i + it) & 7] : f2{1e-3f, 2e-3f});
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc.x += u[i].x + u[i].y;
       }
@@ -694,8 +700,15 @@ int main(int argc, char** argv) {
     rb("half, lag 2, 4 slots, burn 768", teamd(k_team_def<128, 2, 4, 1, 768>, 128));
     rb("frame, lag 1, 2 slots, burn 1536", teamd(k_team_def<256, 1, 2, 1, 1536>, 256));
     rb("half, lag 2, 4 slots, burn 1536", teamd(k_team_def<128, 2, 4, 1, 1536>, 128));
-    rb("frame, lag 1, 2 slots, burn 3072", teamd(k_team_def<256, 1, 2, 1, 3072>, 256));
-    rb("half, lag 2, 4 slots, burn 3072", teamd(k_team_def<128, 2, 4, 1, 3072>, 128));
+  }
+  if (part == 14) {
+    printf("== part M2: the same under a toggling burn (u = -u/2 + random samples)\n");
+    rb("frame, lag 1, 2 slots, tburn 384", teamd(k_team_def<256, 1, 2, 1, 384, 1>, 256));
+    rb("half, lag 2, 4 slots, tburn 384", teamd(k_team_def<128, 2, 4, 1, 384, 1>, 128));
+    rb("frame, lag 1, 2 slots, tburn 768", teamd(k_team_def<256, 1, 2, 1, 768, 1>, 256));
+    rb("half, lag 2, 4 slots, tburn 768", teamd(k_team_def<128, 2, 4, 1, 768, 1>, 128));
+    rb("frame, lag 1, 2 slots, tburn 1152", teamd(k_team_def<256, 1, 2, 1, 1152, 1>, 256));
+    rb("half, lag 2, 4 slots, tburn 1152", teamd(k_team_def<128, 2, 4, 1, 1152, 1>, 128));
   }
   if (part == 11) {
     printf("== part K: k_rdx's protocol at fp16-storage bytes (input, RD and slots halved; frac on 8.6 GB)\n");
