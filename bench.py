@@ -316,22 +316,9 @@ def main():
     sclk_mhz, _ = eng.rdx_clock()
     copy = None
     if not args.no_copy_ceiling:
-        nbytes = d_iq.numel() * d_iq.element_size()
-        d_cp = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
-        eng.copy_device(d_iq, d_cp, nbytes, stream=stream)
-        torch.cuda.synchronize(dev)
-        reps = 5
-        ca, cb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ca.record(stream)
-        for _ in range(reps):
-            eng.copy_device(d_iq, d_cp, nbytes, stream=stream)
-        cb.record(stream)
-        torch.cuda.synchronize(dev)
-        cms = ca.elapsed_time(cb) / reps
-        del d_cp
-        copy = {"ms": round(cms, 4), "bytes": 2 * nbytes, "GBps": round(2 * nbytes / (cms * 1e-3) / 1e9, 1),
-                "what": "16-byte nontemporal copy of the input cube into an RD-sized buffer (k_rdx's in + RD bytes), "
-                        "one thread per 16 bytes, HIP events, same process"}
+        copy = copy_ceiling(eng, d_iq, dev, stream, 5,
+                            "16-byte nontemporal copy of the input cube into an RD-sized buffer (k_rdx's in + RD "
+                            "bytes), one thread per 16 bytes, HIP events, same process")
 
     # ---- roofline ----------------------------------------------------------------
     # path: SURVEY.md 8d config-4 algorithmic bytes per frame (input + RD map +
@@ -618,6 +605,25 @@ def bench_fp16(eng, cfg, F, args, dev, stream, pmc):
     return out, leg
 
 
+def copy_ceiling(eng, src, dev, stream, reps, what):
+    """The HBM copy ceiling of a kernel's bytes in this process on this box:
+    src (a device tensor) copied into a fresh buffer of its size by k_copy16, HIP events over reps."""
+    import torch
+    nbytes = src.numel() * src.element_size()
+    d_cp = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    eng.copy_device(src, d_cp, nbytes, stream=stream)
+    torch.cuda.synchronize(dev)
+    ca, cb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ca.record(stream)
+    for _ in range(reps):
+        eng.copy_device(src, d_cp, nbytes, stream=stream)
+    cb.record(stream)
+    torch.cuda.synchronize(dev)
+    cms = ca.elapsed_time(cb) / reps
+    del d_cp
+    return {"ms": round(cms, 4), "bytes": 2 * nbytes, "GBps": round(2 * nbytes / (cms * 1e-3) / 1e9, 1), "what": what}
+
+
 def bench_config2(eng, args, dev, stream, pmc):
     """BASELINE config 2: 4096 frames x 128 chirps x 512 samples, range FFT only (K1,
     range cube written, fp32), device-resident; its own roofline on K1's event time."""
@@ -653,6 +659,13 @@ def bench_config2(eng, args, dev, stream, pmc):
            "dtype": "f32", "what": "BASELINE config 2: 4096 x 128 x 512 IQ, range FFT only, cube + profile written",
            "roofline": _roof(per, F2, us, pmc_traffic(pmc, K1_NAME, F2), K1_NAME,
                              "K1 k_range (calibration, mean, window, 512-pt range FFT, cube + profile store)", pmc)}
+    if not args.no_copy_ceiling:   # K1's own in-run ceiling: its input copied into a cube-sized buffer
+        cc = copy_ceiling(eng, d_iq, dev, stream, 10,
+                          "16-byte nontemporal copy of the config-2 input into a cube-sized buffer (K1's in + cube "
+                          "bytes), HIP events, same process")
+        out["roofline"]["copy_ceiling_ms"] = cc["ms"]
+        out["roofline"]["frac_of_copy_ceiling"] = round(cc["ms"] / (us * 1e-3), 4)
+        out["roofline"]["copy_ceiling"] = cc
     leg = dict(name="config2", cfg=cfg2, d_iq=d_iq, d_cube=d_cube, d_prof=d_prof)
     return out, leg
 
