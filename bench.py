@@ -42,8 +42,11 @@ STFT_WLEN, STFT_NOVERLAP, STFT_NFFT = 20, 19, 64
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # the first ~20-30 steps of a process run ~1 % slower (k_rdx 4.38 against 4.34 ms; the same at 200
+    # timed steps after 3 warm ones: profiles/r05_bench_warmup.txt), so the default warms up 30 steps
+    # and times 100 (0.45 s of a 4096-frame stream per GPU)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--frames", type=int, default=4096, help="frames per GPU per step")
     ap.add_argument("--fp16", action="store_true", help="config-4 fp16 storage variant")
     ap.add_argument("--chunk", type=int, default=0, help="frames per range/Doppler chunk (0 = library default)")
