@@ -103,24 +103,9 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
     int sel[8];
     float selv[8];
     const int n = select_peaks<NR, false>(q, lane, a.profile + f * NR, sel, selv);
-    float* slow = a.slow_mag + f * C;
-    if (n > 0) {
-      const int row = sel[0], tt = xcd_group(row);
-      const int32_t* ci = a.cand_idx + (f * a.tiles + tt) * a.ncand;
-      int c = -1;
-      for (int i = a.ncand - 1; i >= 0; --i)
-        if (ci[i] == row) c = i;
-      if (c >= 0) {
-        const float* src = a.cand_rows + ((f * a.tiles + tt) * a.ncand + c) * (int64_t)C;
-        for (int k = lane; k < C; k += 64) slow[k] = sqrtf(src[k]);     // candidates hold |X|^2
-      } else {
-        slow_row_direct(a, f, row, lane, slow);                         // wave-uniform branch
-      }
-    } else {
-      for (int k = lane; k < C; k += 64) slow[k] = 0.f;
-    }
     // :233 [val, di] = max(abs(D)) of each target row: from the RD map when it
-    // was written, else from rowpk
+    // was written, else from rowpk.  (Ahead of the slow-time row below: the RD loads and the
+    // candidate-index loads then go out together, before any store of the wave.)
     int2 pkr[8];
     if (a.rd) {
 #pragma unroll
@@ -136,6 +121,22 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
           wave_argmax(bv, bi);
           pkr[j] = make_int2(__float_as_int(bv), bi);
         }
+    }
+    float* slow = a.slow_mag + f * C;
+    if (n > 0) {
+      const int row = sel[0], tt = xcd_group(row);
+      const int32_t* ci = a.cand_idx + (f * a.tiles + tt) * a.ncand;
+      int c = -1;
+      for (int i = a.ncand - 1; i >= 0; --i)
+        if (ci[i] == row) c = i;
+      if (c >= 0) {
+        const float* src = a.cand_rows + ((f * a.tiles + tt) * a.ncand + c) * (int64_t)C;
+        for (int k = lane; k < C; k += 64) slow[k] = sqrtf(src[k]);     // candidates hold |X|^2
+      } else {
+        slow_row_direct(a, f, row, lane, slow);                         // wave-uniform branch
+      }
+    } else {
+      for (int k = lane; k < C; k += 64) slow[k] = 0.f;
     }
     if (lane < M) {
       int ri = 0, di = 0;
