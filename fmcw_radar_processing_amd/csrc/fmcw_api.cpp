@@ -833,12 +833,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   const int slots = fmcw::XCD_MAX_SLOTS;
   {
     CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8));
-    {
-      void* before = c->x_ctr.p;
-      CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
-      // zeroed once: every k_rdx launch leaves its counters at zero (kernels_xcd.hip, exit_count)
-      if (c->x_ctr.p != before) HIPCHK(hipMemsetAsync(c->x_ctr.p, 0, sizeof(unsigned) * fmcw::XCD_CTR_WORDS, s));
-    }
+    CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
     if (!c->x_clk.p) {
       CHK(c->x_clk.ensure(4 * sizeof(unsigned long long)));
       HIPCHK(hipMemsetAsync(c->x_clk.p, 0, 4 * sizeof(unsigned long long), s));

@@ -91,8 +91,7 @@ struct OnePassArgs {
   // XCD-team schedule (k_rdx) only:
   float2* xcube;           // [8 XCDs][slots][XCD_TILES groups][C][32] range-cube hand-off slots
   unsigned* xctr;          // [8 XCDs][2: ready, (unused)][XCD_MAX_SLOTS][32] + [8][32] tickets + the abort word:
-                           // one 128-byte line per counter, XCD_CTR_WORDS in all (zero between launches: the
-                           // launch's last workgroup to exit zeroes [0, XCD_IDLE) and the exit count)
+                           // one 128-byte line per counter, XCD_CTR_WORDS in all (zeroed per launch)
   unsigned* xerr;          // sticky, reported by fmcw_synchronize: bit 0 a hand-off wait timed out, bit 1 an XCD
                            // got more than 32 blocks (the launch's own abort word lets its grid drain; a later
                            // launch starts with a clear one)
@@ -117,8 +116,7 @@ constexpr int XCD_TICKETS = 8 * 2 * 32 * XCD_MAX_SLOTS;   // xctr offset of the 
 constexpr int XCD_ABORT = XCD_TICKETS + 8 * 32;           // xctr offset of the launch's abort word (own line)
 constexpr int XCD_IDLE = XCD_ABORT + 32;                  // xctr offset of [256 CUs][32] words the non-publishing
                                                           // waves add 0 to (kernels_xcd.hip, publish)
-constexpr int XCD_EXIT = XCD_IDLE + 256 * 32;             // xctr offset of the exit count (own line)
-constexpr int XCD_CTR_WORDS = XCD_EXIT + 32;
+constexpr int XCD_CTR_WORDS = XCD_IDLE + 256 * 32;
 // table sections (float2, [..][64 lanes])
 constexpr int XT_R1 = 0;             // [14]: W1024^((2l + e) k1), index 2 (k1 - 1) + e
 constexpr int XT_R2 = 14 * 64;       // [15]: W128^((l & 7) s1), s1 = 1..15

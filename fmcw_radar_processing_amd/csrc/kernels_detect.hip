@@ -103,25 +103,6 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
     int sel[8];
     float selv[8];
     const int n = select_peaks<NR, false>(q, lane, a.profile + f * NR, sel, selv);
-    // :233 [val, di] = max(abs(D)) of each target row: from the RD map when it
-    // was written, else from rowpk.  (Ahead of the slow-time row below: the RD loads and the
-    // candidate-index loads then go out together, before any store of the wave.)
-    int2 pkr[8];
-    if (a.rd) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (j < n) {
-          const int64_t row = (f * NR + sel[j]) * (int64_t)a.ND;
-          float bv = -1.f;
-          int bi = INT_MAX;
-          for (int e = lane; e < a.ND; e += 64) {
-            const float m = sqrtf(cabs2(op::ld_iq(a.rd, row + e, a.rd_h))) * q.rd_unscale;
-            if (m > bv) { bv = m; bi = e; }
-          }
-          wave_argmax(bv, bi);
-          pkr[j] = make_int2(__float_as_int(bv), bi);
-        }
-    }
     float* slow = a.slow_mag + f * C;
     if (n > 0) {
       const int row = sel[0], tt = xcd_group(row);
@@ -137,6 +118,24 @@ __global__ __launch_bounds__(256) void k_detect_1p(Detect1pArgs a) {
       }
     } else {
       for (int k = lane; k < C; k += 64) slow[k] = 0.f;
+    }
+    // :233 [val, di] = max(abs(D)) of each target row: from the RD map when it
+    // was written, else from rowpk
+    int2 pkr[8];
+    if (a.rd) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j < n) {
+          const int64_t row = (f * NR + sel[j]) * (int64_t)a.ND;
+          float bv = -1.f;
+          int bi = INT_MAX;
+          for (int e = lane; e < a.ND; e += 64) {
+            const float m = sqrtf(cabs2(op::ld_iq(a.rd, row + e, a.rd_h))) * q.rd_unscale;
+            if (m > bv) { bv = m; bi = e; }
+          }
+          wave_argmax(bv, bi);
+          pkr[j] = make_int2(__float_as_int(bv), bi);
+        }
     }
     if (lane < M) {
       int ri = 0, di = 0;

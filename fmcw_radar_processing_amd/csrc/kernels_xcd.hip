@@ -203,7 +203,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // ticket drawn on that XCD's counter: 256 blocks give every XCD exactly 32.
   __shared__ int team[2];
   __shared__ unsigned gflag;           // the last step whose ready(j - 1) wave 0 has seen
-  __shared__ unsigned xlast;           // this workgroup was the launch's last to exit
   if (tid == 0) {
     gflag = 0;
     unsigned xcc;
@@ -217,28 +216,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   }
   __syncthreads();
   const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
-  // The launch's counters are zero when it starts and when it ends: every workgroup counts itself
-  // out once it is past its last use of them, and the last one zeroes the ready counters, tickets
-  // and abort word (the idle words only ever receive adds of 0) and the exit count -- a memset
-  // launch before every k_rdx cost the stream ~10 us.  The next launch is ordered after this one
-  // (stream order and the per-device k_rdx chain), so it sees the zeros.
-  auto exit_count = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_s_waitcnt(0);     // every wave's counter operations (publish adds) have completed
-    __syncthreads();
-    typedef __attribute__((address_space(1))) unsigned gu32;
-    if (tid == 0)
-      xlast = __hip_atomic_fetch_add((gu32*)(a.xctr + XCD_EXIT), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-              gridDim.x - 1;
-    __syncthreads();
-    if (xlast) {
-      for (int i = tid; i < XCD_IDLE; i += 64 * NW) __hip_atomic_store((gu32*)(a.xctr + i), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tid == 0) __hip_atomic_store((gu32*)(a.xctr + XCD_EXIT), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-  if (k >= NK) {                       // more than 32 blocks on one XCD: its team is short (waits time out)
-    exit_count();
-    return;
-  }
+  if (k >= NK) return;                 // more than 32 blocks on one XCD: its team is short (waits time out)
   // the effective shader clock of the launch: team 0's member 0 stamps both clocks (vector stores)
   const bool stamper = a.clk != nullptr && x == 0 && k == 0 && tid == 0;
   if (stamper) {
@@ -793,7 +771,6 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     a.clk[2] = __builtin_amdgcn_s_memtime();
     a.clk[3] = __builtin_amdgcn_s_memrealtime();
   }
-  exit_count();
 #ifdef XK_STAMPS
   if (lane == 0 && (w == 0 || w == 4)) {
     unsigned long long* d = a.dbg + ((int64_t)blockIdx.x * 2 + (w >> 2)) * 16;
@@ -844,6 +821,7 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
     (void)hipGetLastError();
     if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
   }
+  if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   if (a.nteams < 1 || a.nteams > 8) return hipErrorInvalidValue;
   const dim3 g(xk::NK * a.nteams), bl(64 * xk::NW);
   // Residency.  The grid (one 512-thread block per CU) is checked against the occupancy query
