@@ -716,7 +716,9 @@ __global__ __launch_bounds__(256) void k_stft64f(StftArgs a, float* __restrict__
         } else {                                                    // :283 20 log10(P / max(P))
           for (int i = lane; i < n4; i += 64) {
             const f4t v = t4[i];
-            reinterpret_cast<f4t*>(out)[i] = f4t{db20(v.x), db20(v.y), db20(v.z), db20(v.w)};
+            // the dB map is the leg's output, not re-read: streamed out with nontemporal stores
+            // (0.5-0.9 us of the pass's 38, profiles/r05_stft_fold.txt)
+            __builtin_nontemporal_store(f4t{db20(v.x), db20(v.y), db20(v.z), db20(v.w)}, reinterpret_cast<f4t*>(out) + i);
           }
           for (int o = 4 * n4 + lane; o < n; o += 64) out[o] = db20(tile[o]);
         }
