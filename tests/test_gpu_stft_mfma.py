@@ -111,3 +111,40 @@ def test_folded_stft64_meets_the_db_bar(engine, monkeypatch, frames, hop, halo, 
     assert sel.mean() > 0.2
     assert np.abs(d1[sel] - dt[sel]).max() <= 1e-3
     assert (d1[~sel] <= -80 + 1e-3).all() and not np.isnan(d1).any()
+
+
+@pytest.mark.parametrize("L", [0, 1, 19, 20, 21, 83, 84, 85, 256])
+def test_folded_stft64_short_signals(engine, monkeypatch, L):
+    """k_stft64f at the edges of its 64-segment units and of the window: no segment (L < 20:
+    nseg 0, max(P) stays 0, nothing written), one segment (L = 20), a unit's worth plus and minus
+    one; both passes (max(P), then the direct dB map) against fp64 at the dB bar."""
+    import torch
+    from oracle import oracle as O
+    monkeypatch.setenv("FMCW_STFT_MFMA", "1")
+    monkeypatch.setenv("FMCW_STFT64_FOLD", "1")
+    rng = np.random.default_rng(L + 5)
+    x = np.abs(rng.standard_normal(PN) * 10 + 3).astype(np.float32)
+    slow = torch.from_numpy(x.reshape(1, PN)).to("cuda")
+    flist = torch.zeros(1, dtype=torch.int32, device="cuda")
+    d_len = torch.tensor([L], dtype=torch.int64, device="cuda")
+    w = O.stft_window("hann")
+    win = torch.from_numpy(w.astype(np.float32)).to("cuda")
+    max_seg = PN
+    out = torch.full((max_seg, 33), np.nan, dtype=torch.float32, device="cuda")
+    pmax = torch.zeros(1, dtype=torch.float32, device="cuda")
+    nseg = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    engine.stft_power_device(slow, flist, d_len, PN, win, WLEN, WLEN - 1, 64, 1250.0, max_seg, None, pmax, nseg)
+    engine.stft_db_direct_device(slow, flist, d_len, PN, win, WLEN, WLEN - 1, 64, 1250.0, max_seg, pmax, out)
+    torch.cuda.synchronize()
+    n = int(nseg.item())
+    got = out.cpu().numpy()
+    assert n == max(0, L - (WLEN - 1))
+    assert np.isnan(got[n:]).all()                                          # nothing past nseg
+    if n == 0:
+        assert float(pmax.item()) == 0.0
+        return
+    dt = _truth_db(x[:L], None, w, 1)
+    d1 = got[:n].astype(np.float64)
+    sel = dt >= -80
+    assert np.abs(d1[sel] - dt[sel]).max() <= 1e-3
+    assert (d1[~sel] <= -80 + 1e-3).all()
