@@ -272,7 +272,7 @@ struct fmcw_ctx {
     int done(hipStream_t st) {
       for (auto& x : es) {
         if (x->s != st) continue;
-        if (!x->done && hipEventCreateWithFlags(&x->done, hipEventDisableTiming) != hipSuccess) {
+        if (!x->done && hipEventCreateWithFlags(&x->done, hipEventDisableTiming | fmcw::kEvDevice) != hipSuccess) {
           (void)hipGetLastError();
           return fail(FMCW_E_HIP, "per-stream scratch: hipEventCreate failed");
         }
@@ -287,8 +287,15 @@ struct fmcw_ctx {
   // STFT 20-tap tables W[nfft/2+1][20] + the 20 taps they were built from, one per stream that
   // asked for one
   PerStream s_tabs;
+  // a table the caller rewrites (any nfft): the entry no longer holds what a cached nfft-64 key
+  // says it holds, so the key is cleared (a later stft_tab64 with the same window rebuilds)
   float2* stft_tab(hipStream_t st, size_t bytes, int* status) {
-    return static_cast<float2*>(s_tabs.get(st, bytes + STFT_TAPS_BYTES, status));
+    float2* t = static_cast<float2*>(s_tabs.get(st, bytes + STFT_TAPS_BYTES, status));
+    if (t) {
+      s_tabs.last->key = nullptr;
+      s_tabs.last->key_n = 0;
+    }
+    return t;
   }
   static constexpr size_t STFT_TAPS_BYTES = 20 * 4;
   // The device calls at nfft 64 (the bench's config-4 STFT, two passes per step) keep the
@@ -297,7 +304,7 @@ struct fmcw_ctx {
   // differ (a window rewritten in place), so the table is rebuilt once, not every pass.
   // *build: the caller must launch k_stft_table into the returned table.
   float2* stft_tab64(hipStream_t st, const float* d_win, int nfft, bool* build, int* status) {
-    float2* t = stft_tab(st, (size_t)(nfft / 2 + 1) * 20 * 8, status);
+    float2* t = static_cast<float2*>(s_tabs.get(st, (size_t)(nfft / 2 + 1) * 20 * 8 + STFT_TAPS_BYTES, status));
     if (!t) return nullptr;
     PerStream::Entry* e = s_tabs.last;
     *build = !(e->key == d_win && e->key_n == nfft);
@@ -364,7 +371,7 @@ struct fmcw_ctx {
       return e;
     }
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&e, fmcw::kEvDevice) != hipSuccess) return nullptr;   // timing pairs
     return e;
   }
 };
@@ -560,11 +567,11 @@ static int ctx_create_one(int32_t device_id, fmcw_ctx** out) {
   for (int i = 0; i < 2; ++i)
     for (hipEvent_t* e : {&c->ev_h2d[i], &c->ev_comp[i], &c->ev_d2h[i]})
       ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
-  for (int i = 0; i < fmcw_ctx::kSlots; ++i)
+  for (int i = 0; i < fmcw_ctx::kSlots; ++i)   // the streams schedule's joins: device scope
     for (hipEvent_t* e : {&c->ev_k1[i], &c->ev_k2[i], &c->ev_k3[i]})
-      ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+      ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming | fmcw::kEvDevice) == hipSuccess;
   for (hipEvent_t* e : {&c->ev_fork, &c->ev_join})
-    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming | fmcw::kEvDevice) == hipSuccess;
   if (!ok) {
     delete c;
     return fail(FMCW_E_HIP, "stream/event creation failed");
@@ -1570,22 +1577,34 @@ static int stft_impl(fmcw_ctx* c, const float* x, int64_t L, const float* win, i
       StageTimer tm(d, 4, s);
       CHK(stft_coarse_max(d, a, s));
       tm.done();
+    } else if (sel_mode) {   // max(P) only, in the table form the listed-bins pass below uses (at nfft 64
+                             // too: P / max(P) of the listed bins then peaks at exactly 0 dB, as in MATLAB)
+      fmcw::StftArgs a{};
+      a.slow_mag = d_x; a.frame_list = d_list; a.len = d_len; a.pn = (int32_t)Ld;
+      a.win = d_win; a.wlen = wlen; a.hop = hop; a.nfft = nf; a.inv_fs = (float)(1.0 / fs);
+      a.max_seg = ns; a.P = nullptr; a.pmax = d->s_pmax.as<float>(); a.nseg_out = d->s_nseg.as<int64_t>();
+      a.table_form = 1;
+      StageTimer tm(d, 4, s);
+      int st = FMCW_OK;
+      float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);
+      CHK(st);
+      HIPCHK(fmcw::launch_stft_table(d_win, nf, tab, s));
+      HIPCHK(fmcw::launch_stft20(a, tab, 1, nullptr, s, 0, (int64_t)(nf / 2 + 1) * 20));
+      CHK(d->stft_tab_done(s));
+      tm.done();
     } else {
       CHK(fmcw_stft_power_device(d, d_x, d_list, d_len, (int32_t)Ld, nullptr, 0, nullptr, d_win, wlen, noverlap, nf, fs, ns,
-                                 sel_mode ? nullptr : d->s_P.as<float>(), d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
+                                 d->s_P.as<float>(), d->s_pmax.as<float>(), d->s_nseg.as<int64_t>(), s));
     }
-    if (sel_mode) {   // second pass: P of the listed bins (the W table of the first pass is reused)
+    if (sel_mode) {   // second pass: P of the listed bins (the W table the first pass built on s is reused)
       fmcw::StftArgs a{};
       a.slow_mag = d_x; a.frame_list = d_list; a.len = d_len;
       a.pn = (int32_t)Ld; a.win = d_win; a.wlen = wlen; a.hop = hop; a.nfft = nf;
       a.inv_fs = (float)(1.0 / fs); a.max_seg = ns; a.bins = reinterpret_cast<int32_t*>(di + o.bins); a.ncol = ncolP;
       StageTimer tm(d, 4, s);
       int st = FMCW_OK;
-      float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table buffer on s,
-      CHK(st);
-      // rebuilt for this call's window: at nfft 64 the first pass may have kept a cached table
-      // (k_stft64m checks it against the window; this pass's kernel does not)
-      if (fmcw::stft64_form(nf)) HIPCHK(fmcw::launch_stft_table(d_win, nf, tab, s));
+      float2* tab = d->stft_tab(s, (size_t)(nf / 2 + 1) * 20 * 8, &st);   // the first pass's table on s (both
+      CHK(st);                                                             // first-pass forms built it for d_win)
       HIPCHK(fmcw::launch_stft20(a, tab, 3, d->s_P.as<float>(), s, (int64_t)(d->s_P.n / 4), (int64_t)(nf / 2 + 1) * 20));
       CHK(d->stft_tab_done(s));
       tm.done();

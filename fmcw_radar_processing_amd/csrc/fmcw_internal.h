@@ -5,6 +5,19 @@
 
 namespace fmcw {
 
+// Flags of the events that only order work on one device (stream joins, per-stream scratch
+// reuse, k_rdx's launch chain, the timing pairs read after a device synchronise): no system-scope
+// release when they are recorded.  A default event's release makes the queue write the L2s back
+// before the next packet runs; behind k_rdx (whose hand-off slots leave dirty lines in every XCD's
+// L2) that showed as 6-19 us of idle GPU after every recorded event (profiles/r06_gaps.txt).
+// The host-pointer path's copy events keep the default (the host reads what they guard).
+// -DFMCW_EV_SYSFENCE restores the default flags (A/B).
+#ifndef FMCW_EV_SYSFENCE
+constexpr unsigned kEvDevice = hipEventDisableSystemFence;
+#else
+constexpr unsigned kEvDevice = 0;
+#endif
+
 struct RangeArgs {
   const void* iq;          // [nchirps][S] complex, dtype in_dtype
   int in_dtype;            // FMCW_C64 / FMCW_C32H
@@ -202,6 +215,8 @@ struct StftArgs {
   int ncol;                // k_stft20 mode 3 / 4: columns in `bins`
   const int32_t* tiles;    // k_stft_mfma mode 1: the 256-segment tiles to cover (device), nullptr = all
   int ntiles;
+  int table_form;          // 1: the table-based k_stft_mfma / k_stft20 even at nfft 64 (the host call's
+                           // max(P) pass, so that it forms P exactly as its listed-bins pass does)
 };
 
 // 20-tap fast path (kernels_stft.hip k_stft20): W table [nfft/2+1][20] from the window,

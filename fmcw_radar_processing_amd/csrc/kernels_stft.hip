@@ -1014,6 +1014,20 @@ hipError_t launch_stft_table(const float* win, int nfft, float2* tab, hipStream_
   return hipGetLastError();
 }
 
+// CUs of a device, queried once per device (the persistent STFT grids are sized by it)
+static int device_cus(int dev) {
+  static std::mutex mu;
+  static std::map<int, int> cus;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cus.find(dev);
+  if (it == cus.end()) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1) n = 256;
+    it = cus.emplace(dev, n).first;
+  }
+  return it->second;
+}
+
 hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* dst, hipStream_t s, int64_t dst_cap,
                          int64_t tab_cap) {
   if (a.max_seg <= 0) return hipSuccess;
@@ -1043,15 +1057,16 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
   // nfft 64 (config 4): P / max(P) on the matrix cores, bit-identical (FMCW_STFT_MFMA=0: VALU)
   const char* mf = std::getenv("FMCW_STFT_MFMA");
   if ((mode == 4 || a.tiles) && mf && mf[0] == '0') return hipErrorInvalidValue;   // matrix-core form only
-  if (stft64_form(a.nfft) && mode <= 2 && !a.tiles) {
+  // k_stft64f / k_stft64m store 16 bytes per lane at out + 33 s0 (s0 a multiple of 64): an output
+  // that is not 16-byte aligned (a caller's slice) takes the table form, whose stores are 4 bytes
+  const float* outp = mode == 0 ? a.P : dst;
+  const bool out16 = mode == 1 || (reinterpret_cast<uintptr_t>(outp) & 15) == 0;
+  if (stft64_form(a.nfft) && mode <= 2 && !a.tiles && !a.table_form && out16) {
     // persistent: a few blocks per CU loop over the tiles (nseg is on the device: the grid covers
     // max_seg's tiles at most, the blocks past the last tile return)
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    }
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    const int cus = device_cus(dev);
     int bpc = 3;
     if (const char* e = std::getenv("FMCW_STFT64_BPC")) bpc = std::max(1, std::min(16, std::atoi(e)));   // A/B
     const char* fe = std::getenv("FMCW_STFT64_FOLD");
@@ -1064,15 +1079,15 @@ hipError_t launch_stft20(const StftArgs& a, const float2* tab, int mode, float* 
                                   : (mode == 0 ? (const void*)k_stft64f<0, false> : mode == 1 ? (const void*)k_stft64f<1, false>
                                                                                               : (const void*)k_stft64f<2, false>);
       static std::mutex mu;
-      static std::map<const void*, int> occ;
+      static std::map<std::pair<int, const void*>, int> occ;   // per (device, instantiation)
       int bpcf;
       {
         std::lock_guard<std::mutex> lk(mu);
-        auto it = occ.find(kf);
+        auto it = occ.find({dev, kf});
         if (it == occ.end()) {
           int n = 0;
           if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kf, 256, 0) != hipSuccess || n < 1) n = 1;
-          it = occ.emplace(kf, n).first;
+          it = occ.emplace(std::make_pair(dev, kf), n).first;
         }
         bpcf = it->second;
       }

@@ -814,12 +814,12 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   std::lock_guard<std::mutex> lk(xcd_chain_mu);
   if (!xcd_chain_ev[dev]) {
-    if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming | kEvDevice)) != hipSuccess) return e;
   } else if (hipStreamWaitEvent(s, xcd_chain_ev[dev], 0) != hipSuccess) {
     // a stale handle (the runtime tore the device's state down, e.g. hipDeviceReset): no
     // earlier launch can still run, so a fresh event restarts the chain
     (void)hipGetLastError();
-    if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming | kEvDevice)) != hipSuccess) return e;
   }
   if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   if (a.nteams < 1 || a.nteams > 8) return hipErrorInvalidValue;

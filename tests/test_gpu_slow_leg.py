@@ -129,12 +129,15 @@ def test_slow_leg_forced_fix_in_wave(engine, monkeypatch):
     assert err.max() <= TOL_FP32_REL_L2, err
 
 
+@pytest.mark.parametrize("fold", ["1", "0"], ids=["k_stft64f", "k_stft64m"])
 @pytest.mark.parametrize("direct", [False, True], ids=["stored_P", "direct_dB"])
-def test_stft64_cached_table_follows_the_window(engine, direct):
+def test_stft64_cached_table_follows_the_window(engine, direct, fold, monkeypatch):
     """The nfft-64 device calls keep their W table while the window pointer is unchanged; a window
-    rewritten in place (same pointer) must still be used: k_stft64m checks the taps stored behind
-    the table and forms its W entries itself when they differ."""
+    rewritten in place (same pointer) must still be used: k_stft64m (FMCW_STFT64_FOLD=0) checks the
+    taps stored behind the table and forms its W entries itself when they differ; k_stft64f (the
+    default) applies the taps to the samples and never reads the table."""
     import torch
+    monkeypatch.setenv("FMCW_STFT64_FOLD", fold)
     dev, s = "cuda", torch.cuda.current_stream()
     rng = np.random.default_rng(4)
     pn, nfr = 256, 9
@@ -174,3 +177,93 @@ def test_stft64_cached_table_follows_the_window(engine, direct):
     np.testing.assert_array_equal(b2, b1)
     assert mb == mb2
 
+
+
+@pytest.mark.parametrize("fold", ["1", "0"], ids=["k_stft64f", "k_stft64m"])
+def test_stft64_table_after_another_nfft_on_the_stream(engine, fold, monkeypatch):
+    """One window pointer, one stream: an nfft-128 call rewrites the stream's table entry, so the
+    next nfft-64 call must not take the entry as its cached nfft-64 table (the key is
+    cleared by every writer).  The nfft-64 result after the detour equals the one before it."""
+    import torch
+    monkeypatch.setenv("FMCW_STFT64_FOLD", fold)
+    dev, s = "cuda", torch.cuda.current_stream()
+    rng = np.random.default_rng(7)
+    pn, nfr = 256, 5
+    slow = torch.from_numpy((np.abs(rng.standard_normal((nfr, pn))) * 30).astype(np.float32)).to(dev)
+    flist = torch.arange(nfr, dtype=torch.int32, device=dev)
+    d_len = torch.tensor([nfr * pn], dtype=torch.int64, device=dev)
+    max_seg = nfr * pn - 19
+    win = torch.tensor(O.stft_window("kaiser"), dtype=torch.float32, device=dev)
+
+    def run(nfft):
+        nb = nfft // 2 + 1
+        pmax = torch.zeros(1, dtype=torch.float32, device=dev)
+        nseg = torch.zeros(1, dtype=torch.int64, device=dev)
+        out = torch.full((max_seg, nb), np.nan, dtype=torch.float32, device=dev)
+        engine.stft_power_device(slow, flist, d_len, pn, win, 20, 19, nfft, 1250.0, max_seg, out, pmax, nseg, stream=s)
+        torch.cuda.synchronize()
+        return out.cpu().numpy(), float(pmax.item())
+
+    a, ma = run(64)
+    run(128)
+    b, mb = run(64)
+    np.testing.assert_array_equal(b, a)
+    assert ma == mb
+    x = slow.cpu().numpy().reshape(-1).astype(np.float64)
+    P = O.spectrogram(x, O.stft_window("kaiser"), 19, 64, 1250.0)[3].T       # [seg][33], float64
+    np.testing.assert_allclose(b, P, rtol=1e-4, atol=1e-6 * float(P.max()))
+
+
+@pytest.mark.parametrize("direct", [False, True], ids=["stored_P", "direct_dB"])
+def test_stft64_unaligned_output(engine, direct):
+    """An output that is not 16-byte aligned (a caller's slice, fmcw.h sets no alignment rule for
+    d_P / d_out) takes the table form instead of the 16-byte stores of k_stft64f / k_stft64m (ADVICE
+    r05): same dB as the aligned call within the fp32 bar, nothing written outside the slice."""
+    import torch
+    dev, s = "cuda", torch.cuda.current_stream()
+    rng = np.random.default_rng(11)
+    pn, nfr = 256, 6
+    slow = torch.from_numpy((np.abs(rng.standard_normal((nfr, pn))) * 30).astype(np.float32)).to(dev)
+    flist = torch.arange(nfr, dtype=torch.int32, device=dev)
+    d_len = torch.tensor([nfr * pn], dtype=torch.int64, device=dev)
+    max_seg = nfr * pn - 19
+    fs = 1250.0
+    win = torch.tensor(O.stft_window("hann"), dtype=torch.float32, device=dev)
+
+    def run(off):
+        pmax = torch.zeros(1, dtype=torch.float32, device=dev)
+        nseg = torch.zeros(1, dtype=torch.int64, device=dev)
+        buf = torch.full((max_seg * 33 + 8,), -7.0, dtype=torch.float32, device=dev)
+        out = buf[off:off + max_seg * 33].view(max_seg, 33)
+        assert (out.data_ptr() % 16 == 0) == (off % 4 == 0)
+        if direct:
+            engine.stft_power_device(slow, flist, d_len, pn, win, 20, 19, 64, fs, max_seg, None, pmax, nseg, stream=s)
+            engine.stft_db_direct_device(slow, flist, d_len, pn, win, 20, 19, 64, fs, max_seg, pmax, out, stream=s)
+        else:
+            engine.stft_power_device(slow, flist, d_len, pn, win, 20, 19, 64, fs, max_seg, out, pmax, nseg, stream=s)
+            engine.stft_db_device(out, nseg, max_seg, 64, fs, pmax, 0, out, stream=s)
+        torch.cuda.synchronize()
+        b = buf.cpu().numpy()
+        return b[off:off + max_seg * 33].reshape(max_seg, 33), np.concatenate([b[:off], b[off + max_seg * 33:]])
+
+    a0, _ = run(0)
+    a1, rest = run(1)
+    assert np.all(rest == -7.0)
+    x = slow.cpu().numpy().reshape(-1).astype(np.float64)
+    ref = O.spectrogram_pipeline(x, 1.0 / fs, O.stft_window("hann"), 19, nfft=64, nbins=0)["intensity"].T
+    sel = ref > -80
+    for a in (a0, a1):
+        assert np.isfinite(a).all()
+        assert np.abs(a[sel] - ref[sel]).max() <= 1e-3
+
+
+def test_host_stft_nfft64_peaks_at_0_dB(engine):
+    """The host call at nfft 64 with the log-frequency output: its max(P) pass and its listed-bins
+    pass form P the same way, so no intensity exceeds 0 dB (MATLAB: P / max(P) <= 1 exactly) beyond
+    the one rounding of P * (1 / max(P)) (< 1e-6 dB), and the peak is near 0 dB."""
+    rng = np.random.default_rng(5)
+    x = (np.abs(rng.standard_normal(40)) * 10).astype(np.float32)  # 2^nextpow2(40) = 64
+    w = O.stft_window("kaiser").astype(np.float32)
+    out = engine.stft(x, w, 19, 1250.0, nfft=0, n_log_bins=1024)
+    assert out["nfft"] == 64
+    assert -3.0 < np.nanmax(out["intensity"]) <= 1e-6
