@@ -73,6 +73,8 @@ def parse():
                     help="skip the in-run HBM copy ceiling of k_rdx's bytes (roofline.copy_ceiling_ms)")
     ap.add_argument("--dry-dist", action="store_true",
                     help="launcher test without a GPU: the ranks meet over gloo and rank 0 prints n_gpus")
+    ap.add_argument("--dry-empty", default="1",
+                    help="--dry-dist: ranks whose slow-time shard is empty at step 0 (comma list)")
     return ap.parse_args()
 
 
@@ -146,10 +148,12 @@ def dry_dist(args, world: int, rank: int) -> None:
     dist.all_reduce(t)
     F, C, h, M = args.frames, 256, STFT_WLEN - 1, 1
 
+    empty = {int(x) for x in args.dry_empty.split(",") if x.strip()}
+
     def shard(r, step):                 # what rank r's device outputs would hold at this step
         g = np.random.default_rng(1000003 * step + r)
         cnt = (g.random(F) < 0.9).astype(np.int32)
-        if r == 1 and step == 0:
+        if r in empty and step == 0:
             cnt[:] = 0                  # an empty slow-time shard: the halo must skip it
         slow = (g.random((F, C)) * 40).astype(np.float32) * cnt[:, None]
         ridx = (g.integers(2, 30, (F, M)) * cnt[:, None]).astype(np.int32)
@@ -182,13 +186,21 @@ def dry_dist(args, world: int, rank: int) -> None:
                                    for a in allsh], 0)
             checks["rows"] &= rows is not None and np.array_equal(rows.numpy(), want)
         checks["steps"] += 1
+    # the fan-out leg of the GPU line (input_fanout), on 2 frames per rank of the step's frame shape
+    fan = None
+    if not args.no_fanout:
+        fan = input_fanout(dist, world, rank, 2, (C, 1024, 2), torch.float32, "cpu",
+                           lambda: dist.barrier(), lambda: None)
     ok = torch.tensor([int(all(v for k, v in checks.items() if k != "steps"))])
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if rank == 0:
-        print(json.dumps({"metric": METRIC, "n_gpus": world, "ranks_reduced": int(t.item()), "dry_dist": True,
-                          "steps": args.steps, "exchange": {**checks, "all_ranks_ok": bool(ok.item())},
-                          "config": config_block(world, args.frames, args.steps)}),
-              flush=True)
+        line = {"metric": METRIC, "n_gpus": world, "ranks_reduced": int(t.item()), "dry_dist": True,
+                "steps": args.steps, "exchange": {**checks, "all_ranks_ok": bool(ok.item()),
+                                                  "empty_shards_step0": sorted(empty)},
+                "config": config_block(world, args.frames, args.steps)}
+        if fan:
+            line["input_fanout"] = dict(fan, dry=True)
+        print(json.dumps(line), flush=True)
     dist.destroy_process_group()
     if not ok.item():
         sys.exit(4)
@@ -389,21 +401,8 @@ def main():
     # ---- input fan-out over xGMI from rank 0 (reported separately, not in value) -----
     fanout = None
     if world > 1 and not args.no_fanout:
-        nf = 256
-        src = torch.empty((world * nf, C, S, 2), dtype=tdt, device=dev) if rank == 0 else None
-        dst = torch.empty((nf, C, S, 2), dtype=tdt, device=dev)
-        parts = list(src.chunk(world)) if rank == 0 else None
-        dist.scatter(dst, parts, src=0)
-        torch.cuda.synchronize(dev)
-        barrier()
-        t1 = time.perf_counter()
-        dist.scatter(dst, parts, src=0)
-        torch.cuda.synchronize(dev)
-        barrier()
-        ft = time.perf_counter() - t1
-        fanout = {"frames_per_rank": nf, "ms": round(ft * 1e3, 3),
-                  "GBps_root_egress": round(world * nf * C * S * esz / ft / 1e9, 1)}
-        del src, dst
+        fanout = input_fanout(dist, world, rank, 256, (C, S, 2), tdt, dev, barrier,
+                              lambda: torch.cuda.synchronize(dev))
 
     extra, legs = {}, []
     if rank == 0 and not args.no_check:
@@ -455,6 +454,26 @@ def main():
     if not ok:
         print("bench.py: the full-size check against the oracle FAILED (see \"checked\")", file=sys.stderr, flush=True)
         sys.exit(1)
+
+
+def input_fanout(dist, world, rank, nf, frame_shape, tdt, dev, barrier, sync) -> dict:
+    """SURVEY 8e collective 1: the host-staged input scattered from rank 0 (nf frames per rank), timed
+    on its own after one untimed scatter; not part of `value` (each rank generates its frames in
+    HBM).  The same call runs over gloo on CPU tensors in --dry-dist."""
+    import torch
+    src = torch.empty((world * nf,) + tuple(frame_shape), dtype=tdt, device=dev) if rank == 0 else None
+    dst = torch.empty((nf,) + tuple(frame_shape), dtype=tdt, device=dev)
+    parts = list(src.chunk(world)) if rank == 0 else None
+    dist.scatter(dst, parts, src=0)
+    sync()
+    barrier()
+    t1 = time.perf_counter()
+    dist.scatter(dst, parts, src=0)
+    sync()
+    barrier()
+    ft = time.perf_counter() - t1
+    nbytes = world * nf * dst[0].numel() * dst.element_size()
+    return {"frames_per_rank": nf, "ms": round(ft * 1e3, 3), "GBps_root_egress": round(nbytes / ft / 1e9, 1)}
 
 
 def exchange_halo(fdist, world, rank, outs, flist, d_len, h):

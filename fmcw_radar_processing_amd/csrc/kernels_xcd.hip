@@ -80,6 +80,13 @@ constexpr int kRdAux = XK_RD_AUX;
 #define XK_NS (2 * XK_LAG)
 #endif
 constexpr int kLag = XK_LAG;
+#ifndef XK_POLLAT
+#define XK_POLLAT 2                    // where wave 0 first polls ready(j - lag) in the step (see the step loop;
+                                       // round 6: 2 -- after R1 and the next frame's loads -- is 3-5 % faster than 0)
+#endif
+#ifndef XK_POLLNB
+#define XK_POLLNB 0                    // A/B: non-blocking looks at the counter before the poll (see the step loop)
+#endif
 static_assert(kLag == 1 || kLag == 2, "poll lag 1 (shipped) or 2");
 constexpr int kNS = XK_NS;            // hand-off slots in use per XCD (2..XCD_MAX_SLOTS; see the step loop)
 static_assert(kNS >= 2 * kLag && kNS <= 4, "slot reuse: seeing ready(j - lag) proves frame j - 2 lag read");
@@ -368,6 +375,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
 #pragma unroll
     for (int i = 0; i < 8; ++i) { z0[i] = v[2 * i]; z1[i] = v[2 * i + 1]; }
+#ifndef XK_NORANGEFFT   // diagnostic A/B (wrong outputs): the range DFTs and twiddles removed, transposes and stores kept
     dft8p(z0);
     dft8p(z1);
 #pragma unroll
@@ -376,11 +384,13 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       z0[k1] = cmul_a(z0[k1], t.xy);
       z1[k1] = cmul_a(z1[k1], t.zw);
     }
+#endif
   };
   c2* const rt = L.u.rt[w];                             // this wave's transpose region (range T1, T2; Doppler TD)
   const int k1 = lane >> 3, a0 = lane & 7, hh = lane & 7;
   // R2: DFT16 over a1 (lane 8 k1 + a0), twiddle W128^(a0 s1)
   auto r_mid = [&](c2 (&u)[16]) __attribute__((always_inline)) {
+#ifndef XK_NORANGEFFT
     dft16p<1>(u);
 #pragma unroll
     for (int s1 = 1; s1 < 16; s1 += 2) {
@@ -388,6 +398,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       u[s1] = cmul_a(u[s1], t.xy);
       if (s1 < 15) u[s1 + 1] = cmul_a(u[s1 + 1], t.zw);
     }
+#endif
   };
   auto r_t2 = [&](const c2 (&u)[16], c2 (&q0)[8], c2 (&q1)[8]) __attribute__((always_inline)) {
 #pragma unroll
@@ -404,8 +415,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   };
   // R3: DFT8 over a0 and the slot stores
   auto r_end = [&](c2 (&q0)[8], c2 (&q1)[8], char* __restrict__ slot) __attribute__((always_inline)) {
+#ifndef XK_NORANGEFFT
     dft8p(q0);
     dft8p(q1);
+#endif
     // bins k1 + 16 hh + 8 e + 128 s2 -> group 4 s2 + 2 e + (k1 >> 2), position lane & 31
     const int c = k * NW + w;
     // slot stores are buffer stores without a cache-policy flag (the only such stores in k_rdx):
@@ -659,6 +672,46 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     stamp(4);
     if (dj) d_cand(fd, xv, x0r, G16);
     stamp(5);
+    // wave 0's poll of ready(j - lag): XK_POLLAT 2 (shipped, round 6) right after R1 and the next frame's
+    // loads, before D3; A/B 0 after D3 (rounds 3-5), 1 after the candidates.  The other waves still wait for
+    // the flag and issue their group loads after D3, and wave 0 polls once more there (one load: the
+    // counter is already there).  Measured (tools/onepass_perf.py, 4096 frames, same box): 0 4.50-4.60 ms,
+    // 1 4.41-4.55, 2 4.29-4.44; 2 with the second poll skipped once the flag is set 4.51, non-blocking
+    // looks before a blocking poll after D3 4.55-4.65 (profiles/r06_poll_ab.txt).  The stamps show the
+    // mechanism: wave 0 waits for the team in its early poll while wave 4, on the same SIMD, runs its R1
+    // and D3 alone (2.58 -> 1.84 us).
+    // (a macro: the same statements in a lambda trip an LLVM aperture-check bug on the gflag store)
+#define XK_POLL()                                                                                                   \
+  do {                                                                                                              \
+    wait_ge(&ready[((j - kLag) % kNS) * 32], (unsigned)(NK * ((j - kLag) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);   \
+    if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
+  } while (0)
+    // non-blocking form (XK_POLLNB bit 0: here, bit 1: after R1): one look at the counter, the flag set
+    // when it is already there; the blocking poll below then only runs when no look saw it
+#define XK_TRY()                                                                                                    \
+  do {                                                                                                              \
+    if (ld_flag(&ready[((j - kLag) % kNS) * 32]) >= (unsigned)(NK * ((j - kLag) / kNS + 1)))                        \
+      if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);       \
+  } while (0)
+    if (XK_POLLAT == 1 && gj && w == 0) XK_POLL();
+    // A/B 3 / 5: a vector load of the counter (global_load_dword sc1) issued here, before the next frame's
+    // chirp loads, so that waiting for it leaves those in flight; read after R1 and the loads (3) or
+    // after D3 (5), the blocking poll only when it fell short
+    unsigned vpoll = 0;
+    if ((XK_POLLAT == 3 || XK_POLLAT == 5) && gj && w == 0) {   // (a plain buffer load with the sc1 policy: an
+                                                                // atomic load makes the compiler wait vmcnt(0) at once)
+      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(&ready[((j - kLag) % kNS) * 32], (short)0, 4, 0x00020000);
+      vpoll = __builtin_amdgcn_raw_buffer_load_b32(rq, 0, 0, 16);
+    }
+#define XK_VCHECK()                                                                                                 \
+  do {                                                                                                              \
+    if (vpoll >= (unsigned)(NK * ((j - kLag) / kNS + 1))) {                                                         \
+      if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);       \
+    } else {                                                                                                        \
+      XK_POLL();                                                                                                    \
+    }                                                                                                               \
+  } while (0)
+    if ((XK_POLLNB & 1) && gj && w == 0) XK_TRY();
     if (rj) r_prep(xin, z0, z1);
     if (next) {                        // R1 freed the chirp registers: the next frame's loads go out
       const int jn = j + 1 < nj ? j + 1 : nj - 1;
@@ -667,13 +720,18 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
       ld_chirp(frame(jn), xin);
     }
+    if (XK_POLLAT == 2 && gj && w == 0) XK_POLL();
+    if (XK_POLLAT == 3 && gj && w == 0) XK_VCHECK();
+    if ((XK_POLLNB & 2) && gj && w == 0) XK_TRY();
     if (dj) d_a(xv, dmu);
     stamp(6);
     if (gj) {   // wave 0 polls ready(j - 1) (scalar: its vector memory operations stay in flight) and
                 // tells the other waves through LDS; then every wave loads its share of group k
       if (w == 0) {
-        wait_ge(&ready[((j - kLag) % kNS) * 32], (unsigned)(NK * ((j - kLag) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);
-        if (lane == 0) *reinterpret_cast<volatile unsigned*>(&gflag) = (unsigned)j;
+        if (XK_POLLAT == 5) XK_VCHECK();
+        else if (XK_POLLNB == 0 || __hip_atomic_load(&gflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)j)
+          XK_POLL();                     // (after an early poll it returns at its first load; without a
+                                         // call here LLVM 20 emits an illegal aperture compare)
       } else {
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }

@@ -57,7 +57,10 @@ def test_gpus_2_names_config5_and_the_frame_total():
 
 
 @pytest.mark.parametrize("args", [["--gpus", "2", "--stream-frames", "65536"],
-                                  ["--gpus", "3", "--frames", "512", "--steps", "2"]])
+                                  ["--gpus", "3", "--frames", "512", "--steps", "2"],
+                                  ["--gpus", "8", "--stream-frames", "65536"],
+                                  ["--gpus", "8", "--frames", "256", "--steps", "2", "--dry-empty", "3,4"]],
+                         ids=["2_ranks_config5", "3_ranks_empty_middle", "8_ranks_config5", "8_ranks_two_empty"])
 def test_dry_dist_runs_the_step_exchange(args):
     """the ranks run exactly the step's collective sequence (bench.exchange_halo
     -> the STFT leg's max(P) all_reduce -> bench.exchange_rows) on CPU tensors of the step's
@@ -69,9 +72,16 @@ def test_dry_dist_runs_the_step_exchange(args):
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     ex = d["exchange"]
     assert ex["all_ranks_ok"] and ex["halo"] and ex["lengths"] and ex["max"] and ex["rows"], ex
-    assert ex["steps"] == d["steps"] and d["n_gpus"] == int(args[1])
-    if "--stream-frames" in args:
-        assert d["config"]["covers_config5_stream"] and d["steps"] == 8
+    n = int(args[1])
+    assert ex["steps"] == d["steps"] and d["n_gpus"] == n
+    if "--stream-frames" in args:                    # the whole config-5 stream: 65,536 / (n x 4096) steps
+        assert d["config"]["covers_config5_stream"] and d["steps"] == 65536 // (n * 4096)
+        assert d["config"]["workload"].startswith("BASELINE config 5")
+        assert d["config"]["parallelism"] == f"frame-shard dp{n}"
+    if "--dry-empty" in args:                        # two adjacent empty shards: rank 2's halo comes from rank 5
+        assert ex["empty_shards_step0"] == [3, 4]
+    fo = d["input_fanout"]                           # the fan-out leg's fields
+    assert fo["dry"] and fo["frames_per_rank"] == 2 and fo["ms"] > 0 and fo["GBps_root_egress"] > 0
 
 
 def test_stream_frames_must_divide():
