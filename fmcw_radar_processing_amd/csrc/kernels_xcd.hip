@@ -84,6 +84,9 @@ constexpr int kLag = XK_LAG;
 #define XK_POLLAT 2                    // where wave 0 first polls ready(j - lag) in the step (see the step loop;
                                        // round 6: 2 -- after R1 and the next frame's loads -- is 3-5 % faster than 0)
 #endif
+#ifndef XK_POLLW
+#define XK_POLLW 1                     // A/B: waves 0 .. XK_POLLW - 1 take the early poll (XK_POLLAT 2) themselves
+#endif
 #ifndef XK_POLLNB
 #define XK_POLLNB 0                    // A/B: non-blocking looks at the counter before the poll (see the step loop)
 #endif
@@ -140,7 +143,10 @@ __device__ __forceinline__ void wait_ge(const unsigned* p, unsigned v, unsigned*
   for (int it = 0; it < (1 << 20); ++it) {
     if (ld_flag(p) >= v) return;
     if ((it & 63) == 63 && ld_flag(abort)) return;
-    __builtin_amdgcn_s_sleep(2);
+#ifndef XK_PSLEEP
+#define XK_PSLEEP 2                    // A/B: s_sleep between two polls (x 64 cycles)
+#endif
+    __builtin_amdgcn_s_sleep(XK_PSLEEP);
   }
   if (threadIdx.x == 0) {   // global atomics (a flat atomic here tripped an LLVM aperture-check bug)
     typedef __attribute__((address_space(1))) unsigned gu32;
@@ -234,6 +240,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   const int nj = a.F > x ? (int)((a.F - x + T - 1) / T) : 0;
   const int S = FULL ? NR : a.S, S2 = S >> 1, NS = a.slots;
   unsigned* ready = a.xctr + (x * 2 + 0) * 32 * XCD_MAX_SLOTS;
+  // slot s's ready counter (round 6 A/B: 4, 8 or 32 replicas, every publish adding to all, a member polling
+  // its own, ran 0-3 % slower: the counter's line is not a hot spot at one poller per CU,
+  // profiles/r06_poll_ab.txt)
+  auto rdy = [&](int s_) __attribute__((always_inline)) -> unsigned* { return &ready[s_ * 32]; };
 #ifdef XK_DONE
   unsigned* done = ready + 32 * XCD_MAX_SLOTS;
 #endif
@@ -661,7 +671,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     // never wait for an atomic
     if (pub)
       if (lane == 0)
-        __hip_atomic_fetch_add(w == 0 ? &ready[((j - 1) % kNS) * 32] : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
+        __hip_atomic_fetch_add(w == 0 ? rdy((j - 1) % kNS) : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
                                w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     stamp(2);
     c2 z0[8], z1[8], u[16];
@@ -683,14 +693,14 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     // (a macro: the same statements in a lambda trip an LLVM aperture-check bug on the gflag store)
 #define XK_POLL()                                                                                                   \
   do {                                                                                                              \
-    wait_ge(&ready[((j - kLag) % kNS) * 32], (unsigned)(NK * ((j - kLag) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);   \
+    wait_ge(rdy((j - kLag) % kNS), (unsigned)(NK * ((j - kLag) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);   \
     if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
   } while (0)
     // non-blocking form (XK_POLLNB bit 0: here, bit 1: after R1): one look at the counter, the flag set
     // when it is already there; the blocking poll below then only runs when no look saw it
 #define XK_TRY()                                                                                                    \
   do {                                                                                                              \
-    if (ld_flag(&ready[((j - kLag) % kNS) * 32]) >= (unsigned)(NK * ((j - kLag) / kNS + 1)))                        \
+    if (ld_flag(rdy((j - kLag) % kNS)) >= (unsigned)(NK * ((j - kLag) / kNS + 1)))                        \
       if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);       \
   } while (0)
     if (XK_POLLAT == 1 && gj && w == 0) XK_POLL();
@@ -700,7 +710,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     unsigned vpoll = 0;
     if ((XK_POLLAT == 3 || XK_POLLAT == 5) && gj && w == 0) {   // (a plain buffer load with the sc1 policy: an
                                                                 // atomic load makes the compiler wait vmcnt(0) at once)
-      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(&ready[((j - kLag) % kNS) * 32], (short)0, 4, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(rdy((j - kLag) % kNS), (short)0, 4, 0x00020000);
       vpoll = __builtin_amdgcn_raw_buffer_load_b32(rq, 0, 0, 16);
     }
 #define XK_VCHECK()                                                                                                 \
@@ -720,7 +730,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
       ld_chirp(frame(jn), xin);
     }
-    if (XK_POLLAT == 2 && gj && w == 0) XK_POLL();
+    if (XK_POLLAT == 2 && gj && w < XK_POLLW) XK_POLL();
     if (XK_POLLAT == 3 && gj && w == 0) XK_VCHECK();
     if ((XK_POLLNB & 2) && gj && w == 0) XK_TRY();
     if (dj) d_a(xv, dmu);
@@ -732,7 +742,7 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
         else if (XK_POLLNB == 0 || __hip_atomic_load(&gflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)j)
           XK_POLL();                     // (after an early poll it returns at its first load; without a
                                          // call here LLVM 20 emits an illegal aperture compare)
-      } else {
+      } else if (XK_POLLW == 1 || XK_POLLAT != 2 || w >= XK_POLLW) {   // (A/B XK_POLLW: waves 1 .. POLLW - 1 polled too)
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }
       ld_group(slot(j - kLag) + (int64_t)k * C * GP * kES, grp, G16);
