@@ -34,8 +34,20 @@ def main(F=4096, reps=20):
     ms, n = e.timing_read()["range_only"]
     byt = F * (cfg.pn * cfg.nts * 8 + cfg.pn * cfg.nr * 8 + cfg.nr * 4)
     us = ms / n * 1e3
+    # the same process's copy of K1's in + cube bytes (bench.py's config-2 copy ceiling, k_copy16)
+    nb = d_iq.numel() * d_iq.element_size()
+    d_cp = torch.empty(nb // 4, dtype=torch.float32, device="cuda")
+    e.copy_device(d_iq, d_cp, nb, stream=s)
+    torch.cuda.synchronize()
+    ca, cb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ca.record(s)
+    for _ in range(reps):
+        e.copy_device(d_iq, d_cp, nb, stream=s)
+    cb.record(s)
+    torch.cuda.synchronize()
+    cus = ca.elapsed_time(cb) / reps * 1e3
     print(f"k1 cfg2 F={F}: {dt * 1e3:.3f} ms/step, K1 {us:.1f} us, {byt / (us * 1e-6) / 1e12:.2f} TB/s "
-          f"(frac {byt / (us * 1e-6) / 8e12:.3f})", flush=True)
+          f"(frac {byt / (us * 1e-6) / 8e12:.3f}), copy {cus:.1f} us (K1 at {cus / us:.3f} of it)", flush=True)
     e.close()
 
 
