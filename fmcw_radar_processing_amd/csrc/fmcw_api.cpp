@@ -897,9 +897,9 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       const char* e = std::getenv("FMCW_ONEPASS_FORCE_FIX");
       a.force_fix = (e && e[0] == '1') ? 1 : 0;
     }
-#ifdef XK_STAMPS
+#if defined(XK_STAMPS) || defined(XK_SKEW)
     static unsigned long long* xdbg = nullptr;
-    if (!xdbg) HIPCHK(hipMalloc(&xdbg, (size_t)1 << 17));
+    if (!xdbg) HIPCHK(hipMalloc(&xdbg, (size_t)1 << 20));
     a.dbg = xdbg;
 #endif
     {
@@ -907,6 +907,51 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       {
         HIPCHK(fmcw::launch_xcd(a, s));
         c->xcd_used = true;
+#ifdef XK_SKEW
+        {   // diagnostic build: the team's skew.  Per XCD and step j: the spread of the 32 members' publish
+            // times of R(j - 1), and how long after the last publish each member's poll of it returned
+            // (100 MHz realtime clock, steps 8 .. 247 of the launch); which member published last how often
+          constexpr int ST = 256;
+          const int nblk = 32 * a.nteams;
+          std::vector<unsigned long long> hh((size_t)nblk * 2 * ST);
+          HIPCHK(hipStreamSynchronize(s));
+          HIPCHK(hipMemcpy(hh.data(), a.dbg, hh.size() * 8, hipMemcpyDeviceToHost));
+          double spread = 0, lag_min = 0, lag_max = 0, lag_mean = 0, pub_to_first_poll = 0;
+          long n = 0;
+          std::vector<long> last(32, 0), first(32, 0);
+          for (int xx = 0; xx < a.nteams; ++xx)
+            for (int j = 8; j < ST - 8; ++j) {
+              unsigned long long pmin = ~0ull, pmax = 0, qmin = ~0ull, qmax = 0;
+              double qs = 0;
+              int kl = 0, kf = 0;
+              for (int kk = 0; kk < 32; ++kk) {
+                const unsigned long long p_ = hh[((size_t)(xx * 32 + kk)) * 2 * ST + 2 * j];
+                const unsigned long long q_ = hh[((size_t)(xx * 32 + kk)) * 2 * ST + 2 * j + 1];
+                if (p_ > pmax) { pmax = p_; kl = kk; }
+                if (p_ < pmin) { pmin = p_; kf = kk; }
+                qmin = std::min(qmin, q_); qmax = std::max(qmax, q_);
+                qs += (double)q_;
+              }
+              if (!pmin || !qmin) continue;
+              spread += (double)(pmax - pmin);
+              lag_min += (double)qmin - (double)pmax;
+              lag_max += (double)qmax - (double)pmax;
+              lag_mean += qs / 32 - (double)pmax;
+              pub_to_first_poll += (double)qmin - (double)pmin;
+              ++last[kl]; ++first[kf]; ++n;
+            }
+          if (n) {
+            std::fprintf(stderr, "xk-skew (us, %ld team-steps): publish spread %.2f | poll return after the last publish: "
+                         "first %.2f mean %.2f last %.2f\n", n, spread / n / 100, lag_min / n / 100, lag_mean / n / 100,
+                         lag_max / n / 100);
+            std::fprintf(stderr, "xk-skew last publisher by member:");
+            for (int kk = 0; kk < 32; ++kk) std::fprintf(stderr, " %ld", last[kk]);
+            std::fprintf(stderr, "\nxk-skew first publisher by member:");
+            for (int kk = 0; kk < 32; ++kk) std::fprintf(stderr, " %ld", first[kk]);
+            std::fprintf(stderr, "\n");
+          }
+        }
+#endif
 #ifdef XK_STAMPS
         {   // diagnostic build: per-step phase times of k_rdx (100 MHz realtime clock), averaged over blocks
           const int nblk = 32 * a.nteams;

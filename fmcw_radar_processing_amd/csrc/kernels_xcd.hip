@@ -84,11 +84,8 @@ constexpr int kLag = XK_LAG;
 #define XK_POLLAT 2                    // where wave 0 first polls ready(j - lag) in the step (see the step loop;
                                        // round 6: 2 -- after R1 and the next frame's loads -- is 3-5 % faster than 0)
 #endif
-#ifndef XK_POLLW
-#define XK_POLLW 1                     // A/B: waves 0 .. XK_POLLW - 1 take the early poll (XK_POLLAT 2) themselves
-#endif
-#ifndef XK_POLLNB
-#define XK_POLLNB 0                    // A/B: non-blocking looks at the counter before the poll (see the step loop)
+#ifndef XK_SKEW_STEPS
+#define XK_SKEW_STEPS 256
 #endif
 static_assert(kLag == 1 || kLag == 2, "poll lag 1 (shipped) or 2");
 constexpr int kNS = XK_NS;            // hand-off slots in use per XCD (2..XCD_MAX_SLOTS; see the step loop)
@@ -351,7 +348,9 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       if constexpr (H) t = __builtin_convertvector(xin[i], f4v);
       else t = xin[i];
 #ifndef XK_NOREF
-      t = __builtin_elementwise_fma(f4v{-dsc, -dsc, -dsc, -dsc}, L.x0[lane + 64 * i], t);   // x - x_0 (exact for near-equal values)
+      // x - x_0 (exact for near-equal values).  (Round 6, fp16 storage: the widening folded into this as
+      // v_fma_mix_f32 took 16 VALU instructions per wave-step out and no time: profiles/r06_fp16_bounds.txt)
+      t = __builtin_elementwise_fma(f4v{-dsc, -dsc, -dsc, -dsc}, L.x0[lane + 64 * i], t);
 #endif
       if constexpr (!FULL)
         if (!(lane + 64 * i < S2)) t = f4v{0.f, 0.f, 0.f, 0.f};
@@ -473,15 +472,23 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       for (int i = 0; i < 4; ++i) {
         const int e = tid + 512 * i;            // 16-byte piece: chirp e >> 3, positions 4 (e & 7) .. + 3
         const u4v u = __builtin_bit_cast(u4v, t[i]);
-        const float2 a0 = h2f(u.x), a1 = h2f(u.y), a2 = h2f(u.z), a3 = h2f(u.w);
         f4v* d = &L.u.stg[(e >> 3) * 17 + (e & 7) * 2];
         // kept as X / Nr: the rows below scale their outputs, the Doppler window the rest
-        const f4v lo = f4v{a0.x, a0.y, a1.x, a1.y}, hi = f4v{a2.x, a2.y, a3.x, a3.y};
         // lanes 4-7 of each 8-lane store group write their upper half first: the group's 8 stores
         // then hit 8 different 16-byte bank groups (conflict-free ds_write_b128)
         const bool sw = (e >> 2) & 1;
+#ifndef XK_ST16SEL
+        // the swap applied to the packed halves before they are widened: 4 selects of 32-bit words
+        // instead of 8 of floats (round 6)
+        const float2 b0 = h2f(sw ? u.z : u.x), b1 = h2f(sw ? u.w : u.y), c0 = h2f(sw ? u.x : u.z), c1 = h2f(sw ? u.y : u.w);
+        d[sw ? 1 : 0] = f4v{b0.x, b0.y, b1.x, b1.y};
+        d[sw ? 0 : 1] = f4v{c0.x, c0.y, c1.x, c1.y};
+#else
+        const float2 a0 = h2f(u.x), a1 = h2f(u.y), a2 = h2f(u.z), a3 = h2f(u.w);
+        const f4v lo = f4v{a0.x, a0.y, a1.x, a1.y}, hi = f4v{a2.x, a2.y, a3.x, a3.y};
         d[sw ? 1 : 0] = sw ? hi : lo;
         d[sw ? 0 : 1] = sw ? lo : hi;
+#endif
       }
     } else {
 #pragma unroll
@@ -673,6 +680,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
       if (lane == 0)
         __hip_atomic_fetch_add(w == 0 ? rdy((j - 1) % kNS) : a.xctr + XCD_IDLE + (x * NK + k) * 32 + w,
                                w == 0 ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#ifdef XK_SKEW     // diagnostic build: when each member published R(j - 1) and when its poll of it returned
+    if (pub && w == 0 && lane == 0 && j < XK_SKEW_STEPS)
+      a.dbg[(int64_t)(x * NK + k) * (2 * XK_SKEW_STEPS) + 2 * j] = __builtin_amdgcn_s_memrealtime();
+#endif
     stamp(2);
     c2 z0[8], z1[8], u[16];
     c2 xv[16], x0r{0.f, 0.f}, dmu{0.f, 0.f};
@@ -686,42 +697,19 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     // loads, before D3; A/B 0 after D3 (rounds 3-5), 1 after the candidates.  The other waves still wait for
     // the flag and issue their group loads after D3, and wave 0 polls once more there (one load: the
     // counter is already there).  Measured (tools/onepass_perf.py, 4096 frames, same box): 0 4.50-4.60 ms,
-    // 1 4.41-4.55, 2 4.29-4.44; 2 with the second poll skipped once the flag is set 4.51, non-blocking
-    // looks before a blocking poll after D3 4.55-4.65 (profiles/r06_poll_ab.txt).  The stamps show the
-    // mechanism: wave 0 waits for the team in its early poll while wave 4, on the same SIMD, runs its R1
-    // and D3 alone (2.58 -> 1.84 us).
+    // 1 4.41-4.55, 2 4.29-4.44.  Not kept (profiles/r06_poll_ab.txt): the second poll skipped once the flag
+    // is set (4.51), non-blocking looks before a blocking poll after D3 (4.55-4.65), a vector sc1 load of the
+    // counter issued before the chirp loads (5.99-6.33), waves 0-1 / 0-3 each polling (5.93 / 9.2), waves
+    // 1-3 sleeping or waves 4-7 prioritised at this point (+1-3 %), 4-32 replicas of the counter (0 to +3 %).
+    // The stamps show the mechanism: wave 0 waits for the team in its early poll while wave 4, on the same
+    // SIMD, runs its R1 and D3 alone (2.58 -> 1.84 us).
     // (a macro: the same statements in a lambda trip an LLVM aperture-check bug on the gflag store)
 #define XK_POLL()                                                                                                   \
   do {                                                                                                              \
     wait_ge(rdy((j - kLag) % kNS), (unsigned)(NK * ((j - kLag) / kNS + 1)), a.xctr + XCD_ABORT, a.xerr);   \
     if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);         \
   } while (0)
-    // non-blocking form (XK_POLLNB bit 0: here, bit 1: after R1): one look at the counter, the flag set
-    // when it is already there; the blocking poll below then only runs when no look saw it
-#define XK_TRY()                                                                                                    \
-  do {                                                                                                              \
-    if (ld_flag(rdy((j - kLag) % kNS)) >= (unsigned)(NK * ((j - kLag) / kNS + 1)))                        \
-      if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);       \
-  } while (0)
     if (XK_POLLAT == 1 && gj && w == 0) XK_POLL();
-    // A/B 3 / 5: a vector load of the counter (global_load_dword sc1) issued here, before the next frame's
-    // chirp loads, so that waiting for it leaves those in flight; read after R1 and the loads (3) or
-    // after D3 (5), the blocking poll only when it fell short
-    unsigned vpoll = 0;
-    if ((XK_POLLAT == 3 || XK_POLLAT == 5) && gj && w == 0) {   // (a plain buffer load with the sc1 policy: an
-                                                                // atomic load makes the compiler wait vmcnt(0) at once)
-      const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(rdy((j - kLag) % kNS), (short)0, 4, 0x00020000);
-      vpoll = __builtin_amdgcn_raw_buffer_load_b32(rq, 0, 0, 16);
-    }
-#define XK_VCHECK()                                                                                                 \
-  do {                                                                                                              \
-    if (vpoll >= (unsigned)(NK * ((j - kLag) / kNS + 1))) {                                                         \
-      if (lane == 0) __hip_atomic_store(&gflag, (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);       \
-    } else {                                                                                                        \
-      XK_POLL();                                                                                                    \
-    }                                                                                                               \
-  } while (0)
-    if ((XK_POLLNB & 1) && gj && w == 0) XK_TRY();
     if (rj) r_prep(xin, z0, z1);
     if (next) {                        // R1 freed the chirp registers: the next frame's loads go out
       const int jn = j + 1 < nj ? j + 1 : nj - 1;
@@ -730,19 +718,19 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
 #endif
       ld_chirp(frame(jn), xin);
     }
-    if (XK_POLLAT == 2 && gj && w < XK_POLLW) XK_POLL();
-    if (XK_POLLAT == 3 && gj && w == 0) XK_VCHECK();
-    if ((XK_POLLNB & 2) && gj && w == 0) XK_TRY();
+    if (XK_POLLAT == 2 && gj && w == 0) XK_POLL();
+#ifdef XK_SKEW
+    if (gj && w == 0 && lane == 0 && j < XK_SKEW_STEPS)
+      a.dbg[(int64_t)(x * NK + k) * (2 * XK_SKEW_STEPS) + 2 * j + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (dj) d_a(xv, dmu);
     stamp(6);
     if (gj) {   // wave 0 polls ready(j - 1) (scalar: its vector memory operations stay in flight) and
                 // tells the other waves through LDS; then every wave loads its share of group k
       if (w == 0) {
-        if (XK_POLLAT == 5) XK_VCHECK();
-        else if (XK_POLLNB == 0 || __hip_atomic_load(&gflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < (unsigned)j)
-          XK_POLL();                     // (after an early poll it returns at its first load; without a
+        XK_POLL();                       // (after the early poll it returns at its first load; without a
                                          // call here LLVM 20 emits an illegal aperture compare)
-      } else if (XK_POLLW == 1 || XK_POLLAT != 2 || w >= XK_POLLW) {   // (A/B XK_POLLW: waves 1 .. POLLW - 1 polled too)
+      } else {
         while (*reinterpret_cast<volatile unsigned*>(&gflag) < (unsigned)j) __builtin_amdgcn_s_sleep(1);
       }
       ld_group(slot(j - kLag) + (int64_t)k * C * GP * kES, grp, G16);
