@@ -187,6 +187,11 @@ int fmcw_process_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, i
                         void* d_rd_map, int32_t out_dtype, int64_t probe_column,
                         float* d_probe_mag, void* stream);
 
+/* Placement (a performance note, not a requirement): the range kernel reads d_iq and writes
+ * d_range_cube at the same time, and on MI355X its time depends on where the two streams sit
+ * relative to each other in HBM -- 748-860 us per 4096 frames of 128 x 512 for 18 byte gaps between
+ * the end of d_iq and the start of d_range_cube (profiles/r06_k1_place.txt).  Carving both from one
+ * allocation with the cube 64 KiB (or 4-16 MiB) past the input's end measured at the fast end. */
 int fmcw_range_fft_device(fmcw_ctx* ctx, const fmcw_params* p, const void* d_iq, int32_t in_dtype,
                           int64_t F, void* d_range_cube, int32_t out_dtype, float* d_range_profile,
                           void* stream);
