@@ -839,7 +839,11 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
   const int TC = tiles * ncand;
   const int slots = fmcw::XCD_MAX_SLOTS;
   {
+#ifdef FMCW_XCUBE_PAD_AB   // A/B (tools/place_probe.py slots): the slot ring FMCW_XCUBE_PAD bytes into a larger buffer
+    CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8 + ((size_t)1 << 30)));
+#else
     CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8));
+#endif
     CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
     if (!c->x_clk.p) {
       CHK(c->x_clk.ensure(4 * sizeof(unsigned long long)));
@@ -888,6 +892,12 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.cand_rows = c->op_crows.as<float>();
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
     a.xcube = c->x_cube.as<float2>(); a.xctr = c->x_ctr.as<unsigned>(); a.xerr = c->x_err.as<unsigned>();
+#ifdef FMCW_XCUBE_PAD_AB
+    if (const char* e = std::getenv("FMCW_XCUBE_PAD")) {
+      const size_t pad = std::min<size_t>((size_t)std::strtoull(e, nullptr, 0), (size_t)1 << 30) & ~(size_t)255;
+      a.xcube = reinterpret_cast<float2*>(c->x_cube.as<char>() + pad);
+    }
+#endif
     a.slots = slots; a.xtab = c->x_tab.as<float2>(); a.cal_sum = c->cal_sum;
     a.clk = c->x_clk.as<unsigned long long>();
     a.s16mask = h ? host_s16mask(p, NR) : 0u;
