@@ -1,6 +1,6 @@
 """k_rdx (and K1) against the allocation kind of the streams it reads once and writes once (probe).
 
-python tools/uc_probe.py -> one line per combination of the input cube and the output (RD map for k_rdx,
+python tools/uc_probe.py [which in out reps] -> one line per combination of the input cube and the output (RD map for k_rdx,
 range cube for K1) allocated by torch (default: coarse-grained, cached in the L2) or by
 hipExtMallocWithFlags(hipDeviceMallocUncached): uncached lines never enter the XCD's L2, so they cannot
 evict k_rdx's hand-off slots (the slots' write-backs are 7.9 of the 16.4 GB written).
@@ -35,10 +35,15 @@ def alloc(n_floats, flag):
     return torch.as_tensor(_Dev(p.value, n_floats), device="cuda"), p
 
 
-def main(F=4096, reps=10):
+KIND = {"default": None, "uncached": UNCACHED, "contiguous": CONTIG}
+
+
+def main(F=4096, reps=10, only=None, combos=None):
+    """only / combos: one kernel and one (in, out) pair, for a rocprofv3 --pmc pass (tools/uc_pmc.sh)."""
     e = Engine(0)
     s = torch.cuda.current_stream()
-    for which in ("rdx", "k1"):
+    combos = combos or ((None, None), (UNCACHED, None), (None, UNCACHED), (UNCACHED, UNCACHED), (CONTIG, CONTIG))
+    for which in (only,) if only else ("rdx", "k1"):
         cfg = P.config(4 if which == "rdx" else 2)
         e.set_taps(cfg, P.synth_calibration(cfg.nts))
         n_in = F * cfg.pn * cfg.nts * 2
@@ -49,8 +54,8 @@ def main(F=4096, reps=10):
                     tgt_range_mag=torch.empty((F, M), device="cuda"),
                     tgt_doppler_idx=torch.empty((F, M), dtype=torch.int32, device="cuda"),
                     slow_mag=torch.empty((F, cfg.pn), device="cuda"))
-        for rnd in range(2):
-            for fin, fout in ((None, None), (UNCACHED, None), (None, UNCACHED), (UNCACHED, UNCACHED), (CONTIG, CONTIG)):
+        for rnd in range(1 if only else 2):
+            for fin, fout in combos:
                 t_in, p_in = alloc(n_in, fin)
                 t_out, p_out = alloc(n_out, fout)
                 d_in = t_in.view(F, cfg.pn, cfg.nts, 2)
@@ -84,4 +89,7 @@ def main(F=4096, reps=10):
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1:
+        main(reps=int(sys.argv[4]), only=sys.argv[1], combos=((KIND[sys.argv[2]], KIND[sys.argv[3]]),))
+    else:
+        main()
