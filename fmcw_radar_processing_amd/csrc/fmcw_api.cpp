@@ -787,6 +787,10 @@ static int build_xcd_tab(fmcw_ctx* c, hipStream_t s) {
       for (int e = 0; e < 2; ++e) xput(fmcw::XT_R1 + (2 * (k1 - 1) + e) * 64 + l, (2 * l + e) * k1);   // W1024^(a k1)
     for (int s1 = 1; s1 < 16; ++s1) xput(fmcw::XT_R2 + (s1 - 1) * 64 + l, 8 * ((l & 7) * s1));      // W128^(a0 s1)
     for (int d0 = 1; d0 < 16; ++d0) xput(fmcw::XT_D1 + (d0 - 1) * 64 + l, 4 * ((l & 15) * d0));     // W256^(q d0)
+    // half-frame build (-DXK_HALF)
+    for (int k1 = 1; k1 < 8; ++k1) xput(fmcw::XT_H1 + (k1 - 1) * 64 + l, 2 * l * k1);              // W512^(l k1)
+    for (int s1 = 1; s1 < 8; ++s1) xput(fmcw::XT_H2 + (s1 - 1) * 64 + l, 16 * ((l & 7) * s1));     // W64^(l0 s1)
+    for (int s2 = 0; s2 < 8; ++s2) xput(fmcw::XT_HC + s2 * 64 + l, l + 64 * s2);                   // W1024^(l + 64 s2)
   }
   CHK(c->x_tab.ensure(xt.size() * 4));
   HIPCHK(hipMemcpyAsync(c->x_tab.p, xt.data(), xt.size() * 4, hipMemcpyHostToDevice, s));

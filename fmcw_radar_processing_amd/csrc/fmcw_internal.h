@@ -134,7 +134,13 @@ constexpr int XCD_CTR_WORDS = XCD_IDLE + 256 * 32;
 constexpr int XT_R1 = 0;             // [14]: W1024^((2l + e) k1), index 2 (k1 - 1) + e
 constexpr int XT_R2 = 14 * 64;       // [15]: W128^((l & 7) s1), s1 = 1..15
 constexpr int XT_D1 = 29 * 64;       // [15]: W256^((l & 15) d0), d0 = 1..15
-constexpr int XT_SIZE = 44 * 64;
+// the half-frame hand-off build (-DXK_HALF, kernels_xcd.hip): a wave pair per chirp, each wave a
+// 512-point FFT of the even (odd) samples, combined across the pair
+constexpr int XT_H1 = 44 * 64;       // [7]: W512^(l k1), k1 = 1..7
+constexpr int XT_H2 = 51 * 64;       // [7]: W64^((l & 7) s1), s1 = 1..7
+constexpr int XT_HC = 58 * 64;       // [8]: W1024^(l + 64 s2), s2 = 0..7
+constexpr int XT_SIZE = 66 * 64;
+#ifndef XK_HALF
 // group g, position p (0..31) <-> range bin: r = k1 + 16 h + 8 e + 128 s2 with
 // k1 = (p >> 3) + 4 (g & 1), h = p & 7, e = (g >> 1) & 1, s2 = g >> 2
 __host__ __device__ inline int xcd_bin(int g, int p) {
@@ -142,6 +148,12 @@ __host__ __device__ inline int xcd_bin(int g, int p) {
 }
 __host__ __device__ inline int xcd_group(int r) { return ((r >> 2) & 1) | (((r >> 3) & 1) << 1) | ((r >> 7) << 2); }
 __host__ __device__ inline int xcd_pos(int r) { return ((r & 3) << 3) | ((r >> 4) & 7); }
+#else
+// half-frame build: group g holds bins 32 g .. 32 g + 31 in order
+__host__ __device__ inline int xcd_bin(int g, int p) { return 32 * g + p; }
+__host__ __device__ inline int xcd_group(int r) { return r >> 5; }
+__host__ __device__ inline int xcd_pos(int r) { return r & 31; }
+#endif
 
 struct Detect1pArgs {
   const float* profile;    // [F][NR]

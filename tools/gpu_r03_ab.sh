@@ -9,7 +9,7 @@ if [ -x tools/copy_probe.bin ] && [ "${NOCOPY:-0}" != "1" ]; then
   cat gpurun_out/copy_probe.log; [ $rc -ne 0 ] && { echo "copy probe rc=$rc"; exit $rc; }
 fi
 for n in ${TESTS:-$names}; do
-  FMCW_LIB=ab/$n.so timeout -k 10 300 python -u -m pytest tests/test_gpu_onepass.py -q -x -k xcd --timeout 120 \
+  FMCW_LIB=ab/$n.so timeout -k 10 300 python -u -m pytest tests/test_gpu_onepass.py -q -x -k "${KEXPR:-xcd}" --timeout 120 \
     --timeout-method thread > gpurun_out/abt_$n.log 2>&1; rc=$?
   echo "$n tests rc=$rc: $(tail -1 gpurun_out/abt_$n.log)"
   [ $rc -ne 0 ] && { tail -30 gpurun_out/abt_$n.log; exit $rc; }
@@ -24,7 +24,7 @@ for i in $(seq $N); do
   for n in $names; do
     echo -n "$n: "
     FMCW_LIB=ab/$n.so timeout -k 10 120 python -u tools/onepass_perf.py 4096 20 xcd > gpurun_out/ab_$n.log 2>&1 || { tail -5 gpurun_out/ab_$n.log; exit 1; }
-    grep -E "^xcd| onepass |xk-stamps" gpurun_out/ab_$n.log | tr -s ' ' | tr '\n' ' '; echo
+    grep -E "^xcd| onepass |xk-stamps|sclk" gpurun_out/ab_$n.log | tr -s ' ' | tr '\n' ' '; echo
   done
 done
 for i in $(seq $N); do

@@ -56,6 +56,9 @@ def main(F=4096, reps=10, which="streams,onepass"):
             e.process_device(d_iq, F, dt, outs, d_rd=d_rd, out_dtype=dt, stream=s)
         tm = e.timing_read()
         e.timing(0)
+        if name == "xcd":
+            mhz, us = e.rdx_clock()
+            print(f"   sclk {mhz:.0f} MHz (last k_rdx, {us:.0f} us stamped)", flush=True)
         for k, (ms, n) in tm.items():
             if n:
                 print(f"   {k:14s} {ms / reps:8.3f} ms/step  launches/step {n / reps:.0f}  avg {ms / n * 1e3:.1f} us",
