@@ -87,7 +87,71 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
   for (int m = 0; m < (PROFILE ? P : 1); ++m) pm[m] = 0.f;
 
   float2 cur[P];
+#ifdef K1_GLDS
+  // A/B (round 6): the next chirp of every team of the wave is brought into a wave-private LDS buffer by
+  // LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction) while this chirp is transformed, so its
+  // bytes are in flight without registers; the twiddles are read from an LDS copy (an ordinary global load
+  // behind an LDS-DMA would make the compiler drain it).  Full chirps of c64 samples only (S == NR, 128 <=
+  // NR <= 1024: a chirp is whole 1 KiB pieces and a team lives in one wave).
+  constexpr bool kGlds = std::is_same_v<TIn, float2> && NR >= 128 && NR <= 1024;
+  constexpr int kPiece = NR >= 128 ? NR / 128 : 1;             // 1 KiB pieces per chirp
+  __shared__ __attribute__((aligned(16))) float2 pf[kGlds ? 4 * 64 * P : 1];
+  __shared__ float2 twl[kGlds ? NR : 1];
+  const int wv = threadIdx.x >> 6, ln = threadIdx.x & 63, tiw = (threadIdx.x & 63) / T;   // team in the wave
+  const bool glds = kGlds && a.S == NR;
+  auto glds_issue = [&](int c) __attribute__((always_inline)) {   // chirp c of every team of this wave
+#pragma unroll
+    for (int pc = 0; pc < 8; ++pc) {
+      const int s = pc / kPiece;                                // wave-uniform: the piece's team
+      const int64_t gs = ((int64_t)blockIdx.x * TEAMS + wv * (64 / T) + s) * a.cpt + c;
+      const float2* src = reinterpret_cast<const float2*>(in) + (gs < a.nchirps ? gs : 0) * a.S + (pc % kPiece) * 128 + 2 * ln;
+      // as inline asm: hipcc's own bookkeeping of a builtin LDS-DMA waits vmcnt(0) before every ds_read of the
+      // FFT (it cannot tell pf from the exchange buffer), draining the prefetch; the waits here are explicit
+      typedef __attribute__((address_space(3))) float2 lf2;
+      const unsigned dst = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(lf2*)&pf[wv * 64 * P + pc * 128]);
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+    }
+  };
+  if constexpr (kGlds) {
+    if (glds) {
+      for (int i = threadIdx.x; i < NR; i += 256) twl[i] = a.tw[i];
+      __syncthreads();
+      glds_issue(0);
+    }
+  }
+  if (!glds)
+#endif
   chirp_load<NR>(in + (g0 < a.nchirps ? g0 : 0) * a.S, g0 < a.nchirps, nmax, t0, cur);
+#ifdef K1_GLDS
+  // a loop of its own: sharing the register-load loop would make the compiler wait for that path's
+  // (never pending) chirp loads before every ds_read into the same registers
+  if (kGlds && glds) {
+    for (int c = 0; c < a.cpt; ++c) {
+      const int64_t g = g0 + c;
+      const bool valid = g < a.nchirps;
+      int t = t0;
+      asm volatile("" : "+v"(t));
+      float2 tb[FftPasses<NR>::NB];
+      // chirp c's DMA is the oldest VMEM operation after the previous chirp's stores (P of them when that
+      // chirp was valid): wait for it, read this thread's samples, retire the reads, then reuse the buffer
+      if (c > 0 && g - 1 < a.nchirps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      load_tw_bases<NR>(tb, t, twl);
+#pragma unroll
+      for (int m = 0; m < P; ++m) cur[m] = pf[wv * 64 * P + tiw * NR + t + T * m];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (c + 1 < a.cpt) glds_issue(c + 1);
+      chirp_finish<NR>(cur, in + (valid ? g : 0) * a.S, valid, out + g * NR, a.S, taps, a.cal_sum, a.cube_scale, tb,
+                       my, myred, t);
+      if constexpr (PROFILE) {
+#pragma unroll
+        for (int m = 0; m < P; ++m) pm[m] = fmaxf(pm[m], cabs2(cur[m]));
+      }
+    }
+  } else
+#endif
   for (int c = 0; c < a.cpt; ++c) {
     const int64_t g = g0 + c;
     const bool valid = g < a.nchirps;
@@ -97,8 +161,8 @@ __global__ __launch_bounds__(256, NR >= 2048 ? 2 : K1_WAVES) void k_range(RangeA
     int t = t0;
     asm volatile("" : "+v"(t));
     float2 tb[FftPasses<NR>::NB];
-    load_tw_bases<NR>(tb, t, a.tw);                            // before the prefetch below
     const bool vn = (c + 1 < a.cpt) && (g + 1 < a.nchirps);
+    load_tw_bases<NR>(tb, t, a.tw);                            // before the prefetch below
 #ifndef K1_PREFETCH   // the next chirp is loaded after this one's stores; the other waves of the SIMD cover it
     chirp_finish<NR>(cur, in + (valid ? g : 0) * a.S, valid, out + g * NR, a.S, taps, a.cal_sum, a.cube_scale, tb,
                      my, myred, t);
