@@ -1002,6 +1002,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
   // so the Doppler ends two frames behind the range FFT, as in the frame build.  Slot reuse: R(h) rewrites
   // half slot h mod kNS after this member saw ready(h - lag); the members' loads of R(h - 2 lag) were issued
   // before their slot stores of R(h - lag), so kNS = 2 lag half slots suffice (the frame build's argument).
+  (void)ld_chirp;                                              // the frame build's pieces, unused here
+  (void)ld_group;
+  (void)slot;
+  (void)stamp;
   constexpr int64_t kHalfSlot = (int64_t)NK * (C / 2) * GP * kES;
   auto hslot = [&](int h) __attribute__((always_inline)) { return slots0 + (int64_t)(h % kNS) * kHalfSlot; };
   constexpr int kRDs = RD ? 16 : 1;
