@@ -328,6 +328,7 @@ struct fmcw_ctx {
   int xcd_teams = -1;                          // census of the device: its XCD teams (-1 not run yet, 0 none)
   int8_t xcc_team[16] = {};                    // HW_REG_XCC_ID -> team
   bool xcd_used = false;                       // a k_rdx launch since the last error check
+  int x_ctr_set = 0;                           // the counter set (0 / 1) of x_ctr the next k_rdx launch counts in
   bool x_tab_ok = false;                       // x_tab built for the current taps
   // Multi-device context (fmcw_ctx_create with n_devices > 1): this object is
   // device 0 of the context and peers[i] a full context on device i + 1.  The
@@ -848,7 +849,11 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
 #else
     CHK(c->x_cube.ensure((size_t)8 * slots * fmcw::XCD_TILES * C * 32 * 8));
 #endif
-    CHK(c->x_ctr.ensure(sizeof(unsigned) * fmcw::XCD_CTR_WORDS));
+    if (!c->x_ctr.p) {                         // two counter sets, both zero before the first launch
+      CHK(c->x_ctr.ensure(sizeof(unsigned) * 2 * fmcw::XCD_CTR_WORDS));
+      HIPCHK(hipMemsetAsync(c->x_ctr.p, 0, sizeof(unsigned) * 2 * fmcw::XCD_CTR_WORDS, s));
+      c->x_ctr_set = 0;
+    }
     if (!c->x_clk.p) {
       CHK(c->x_clk.ensure(4 * sizeof(unsigned long long)));
       HIPCHK(hipMemsetAsync(c->x_clk.p, 0, 4 * sizeof(unsigned long long), s));
@@ -895,7 +900,12 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
     a.cand_idx = c->op_cidx.as<int32_t>();
     a.cand_rows = c->op_crows.as<float>();
     a.range_thr = p->range_thr; a.min_d = p->min_d; a.max_d = p->max_d; a.dist_per_bin = p->dist_per_bin;
-    a.xcube = c->x_cube.as<float2>(); a.xctr = c->x_ctr.as<unsigned>(); a.xerr = c->x_err.as<unsigned>();
+    // counter sets: this launch counts in set x_ctr_set and zeroes the other one for the next launch (launches
+    // of a device run one at a time, launch_xcd's chain); FMCW_XCD_MEMSET=1: set 0 and a memset per launch
+    const bool xmemset = [] { const char* e = std::getenv("FMCW_XCD_MEMSET"); return e && e[0] == '1'; }();
+    a.xcube = c->x_cube.as<float2>(); a.xerr = c->x_err.as<unsigned>();
+    a.xctr = c->x_ctr.as<unsigned>() + (xmemset ? 0 : c->x_ctr_set * fmcw::XCD_CTR_WORDS);
+    a.xclr = xmemset ? nullptr : c->x_ctr.as<unsigned>() + (1 - c->x_ctr_set) * fmcw::XCD_CTR_WORDS;
 #ifdef FMCW_XCUBE_PAD_AB
     if (const char* e = std::getenv("FMCW_XCUBE_PAD")) {
       const size_t pad = std::min<size_t>((size_t)std::strtoull(e, nullptr, 0), (size_t)1 << 30) & ~(size_t)255;
@@ -921,6 +931,7 @@ static int process_onepass(fmcw_ctx* c, const fmcw_params* p, const void* d_iq, 
       {
         HIPCHK(fmcw::launch_xcd(a, s));
         c->xcd_used = true;
+        if (a.xclr && nf > 0) c->x_ctr_set ^= 1;   // the next launch counts in the set this one zeroed
 #ifdef XK_SKEW
         {   // diagnostic build: the team's skew.  Per XCD and step j: the spread of the 32 members' publish
             // times of R(j - 1), and how long after the last publish each member's poll of it returned

@@ -104,7 +104,10 @@ struct OnePassArgs {
   // XCD-team schedule (k_rdx) only:
   float2* xcube;           // [8 XCDs][slots][XCD_TILES groups][C][32] range-cube hand-off slots
   unsigned* xctr;          // [8 XCDs][2: ready, (unused)][XCD_MAX_SLOTS][32] + [8][32] tickets + the abort word:
-                           // one 128-byte line per counter, XCD_CTR_WORDS in all (zeroed per launch)
+                           // one 128-byte line per counter, XCD_CTR_WORDS in all (zero when a launch starts)
+  unsigned* xclr;          // the context's other counter set (launches alternate between two): k_rdx's block 0
+                           // zeroes its first XCD_IDLE words for the next launch, which saves a memset packet per
+                           // launch; nullptr: launch_xcd zeroes xctr before the launch (FMCW_XCD_MEMSET=1)
   unsigned* xerr;          // sticky, reported by fmcw_synchronize: bit 0 a hand-off wait timed out, bit 1 an XCD
                            // got more than 32 blocks (the launch's own abort word lets its grid drain; a later
                            // launch starts with a clear one)

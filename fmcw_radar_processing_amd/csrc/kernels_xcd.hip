@@ -236,6 +236,10 @@ __global__ __launch_bounds__(512, 1) void k_rdx(OnePassArgs a) {
     team[1] = kk;
   }
   __syncthreads();
+  // the other counter set, for the next launch (nothing reads it during this one; vector stores, visible to
+  // the next launch at the kernel boundary like a memset's).  The idle words only ever receive + 0.
+  if (a.xclr && blockIdx.x == 0)
+    for (int i = tid; i < XCD_IDLE; i += 512) a.xclr[i] = 0u;
   const int x = __builtin_amdgcn_readfirstlane(team[0]), k = __builtin_amdgcn_readfirstlane(team[1]);
   if (k >= NK) return;                 // more than 32 blocks on one XCD: its team is short (waits time out)
   // the effective shader clock of the launch: team 0's member 0 stamps both clocks (vector stores)
@@ -1207,7 +1211,9 @@ hipError_t launch_xcd(const OnePassArgs& a, hipStream_t s) {
     (void)hipGetLastError();
     if ((e = hipEventCreateWithFlags(&xcd_chain_ev[dev], hipEventDisableTiming | kEvDevice)) != hipSuccess) return e;
   }
-  if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
+  // the counters start at zero: zeroed by the previous launch's block 0 (a.xclr of that launch), or here
+  if (!a.xclr)
+    if ((e = hipMemsetAsync(a.xctr, 0, sizeof(unsigned) * XCD_CTR_WORDS, s)) != hipSuccess) return e;
   if (a.nteams < 1 || a.nteams > 8) return hipErrorInvalidValue;
   const dim3 g(xk::NK * a.nteams), bl(64 * xk::NW);
   // Residency.  The grid (one 512-thread block per CU) is checked against the occupancy query

@@ -7,8 +7,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for r in ${ROUNDS:-1 2}; do for n in ${AB:-base new}; do
-  lib=ab/$n.so; [ "$n" = cur ] && lib=fmcw_radar_processing_amd/libfmcw.so
-  FMCW_LIB=$lib timeout -k 10 300 python3 -u bench.py --cpu-seconds 0 --no-host-path "$@" > gpurun_out/abb_${n}_$r.log 2>&1 || { echo "$n failed"; tail -5 gpurun_out/abb_${n}_$r.log; exit 1; }
+  # a name is a library (ab/<name>.so, cur = in-tree), optionally +VAR=value for one environment setting
+  lib=${n%%+*}; envset=; [ "$lib" != "$n" ] && envset=${n#*+}
+  [ "$lib" = cur ] && lib=fmcw_radar_processing_amd/libfmcw.so || lib=ab/$lib.so
+  env $envset FMCW_LIB=$lib timeout -k 10 300 python3 -u bench.py --cpu-seconds 0 --no-host-path "$@" > gpurun_out/abb_${n}_$r.log 2>&1 || { echo "$n failed"; tail -5 gpurun_out/abb_${n}_$r.log; exit 1; }
   python3 - gpurun_out/abb_${n}_$r.log $n $r <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]).read().splitlines() if l.startswith("{")][-1]); r = d["roofline"]
