@@ -75,6 +75,15 @@ def test_rdx_beside_a_resident_kernel(engine, monkeypatch, hold_s, coop):
         except FmcwError as e:
             assert e.status == _lib.FMCW_E_HIP and "timed out" in str(e), e
             print(f"hold {hold_s} s: FMCW_E_HIP after {wall:.2f} s ({e})")
+            # the launches after a timed-out one start from clean counters (two counter sets per context,
+            # each launch zeroing the other, kernels_xcd.hip): two undisturbed runs equal the reference
+            for _ in range(2):
+                again = _run(engine, cfg, d_iq, s_main)
+                torch.cuda.synchronize()
+                engine.synchronize()
+                again = _host(*again)
+                for k in ref:
+                    np.testing.assert_array_equal(again[k], ref[k], err_msg=k)
             return
         got = _host(*got)
         for k in ref:
